@@ -1,0 +1,199 @@
+"""Generate golden vectors from the REFERENCE PipelineDP LocalBackend.
+
+CONTAINER-ONLY TEST INFRASTRUCTURE.  Run in the build container (where
+/root/reference exists) as
+
+    PYTHONDONTWRITEBYTECODE=1 python oracle/gen_golden.py
+
+It puts oracle/pydp_stub (identity noise, keep-all selection; PyDP is not
+installed) and /root/reference on sys.path, runs the reference
+``DPEngine(..., LocalBackend()).aggregate`` on seeded inputs and writes the
+inputs plus the reference outputs to tests/golden/*.npz.  The fixtures are
+data only; no reference source travels with them.
+
+Cases use non-binding bounds (or deterministic clipping) so that the
+LocalBackend result is deterministic, except ``binding_*`` which records the
+mean of the reference output over many numpy seeds (a distributional target
+for uniform sampling without replacement).
+"""
+import json
+import os
+import sys
+
+sys.dont_write_bytecode = True
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+REF = "/root/reference"
+sys.path.insert(0, os.path.join(HERE, "pydp_stub"))
+sys.path.insert(0, REF)
+
+import numpy as np  # noqa: E402
+
+import pipeline_dp  # noqa: E402  (the reference, via the stub)
+
+OUT = os.path.join(REPO, "tests", "golden")
+
+METRIC = {
+    "count": pipeline_dp.Metrics.COUNT,
+    "sum": pipeline_dp.Metrics.SUM,
+    "mean": pipeline_dp.Metrics.MEAN,
+    "variance": pipeline_dp.Metrics.VARIANCE,
+    "privacy_id_count": pipeline_dp.Metrics.PRIVACY_ID_COUNT,
+}
+
+
+def run_reference(pid, pk, value, cfg, public=None, seed=None):
+    if seed is not None:
+        np.random.seed(seed)
+    acct = pipeline_dp.NaiveBudgetAccountant(total_epsilon=cfg.get("eps", 1.0),
+                                             total_delta=cfg.get("delta", 1e-6))
+    engine = pipeline_dp.DPEngine(acct, pipeline_dp.LocalBackend())
+    kw = dict(metrics=[METRIC[m] for m in cfg["metrics"]],
+              noise_kind=pipeline_dp.NoiseKind(cfg.get("noise_kind", "laplace")),
+              max_partitions_contributed=cfg["L0"],
+              max_contributions_per_partition=cfg["Linf"])
+    for k in ("min_value", "max_value", "min_sum_per_partition", "max_sum_per_partition"):
+        if cfg.get(k) is not None:
+            kw[k] = cfg[k]
+    enforced = cfg.get("already_enforced", False)
+    kw["contribution_bounds_already_enforced"] = enforced
+    params = pipeline_dp.AggregateParams(**kw)
+    has_value = value is not None
+    rows = [(int(pid[i]) if pid is not None else None, int(pk[i]),
+             float(value[i]) if has_value else None) for i in range(len(pk))]
+    ex = pipeline_dp.DataExtractors(
+        privacy_id_extractor=None if enforced else (lambda r: r[0]),
+        partition_extractor=lambda r: r[1],
+        value_extractor=lambda r: r[2])
+    report = pipeline_dp.ExplainComputationReport()
+    res = engine.aggregate(rows, params, ex, public_partitions=public,
+                           out_explain_computaton_report=report)
+    acct.compute_budgets()
+    res = list(res)
+    text = report.text()
+    if not res:
+        return np.zeros(0, np.int64), np.zeros((0, 0)), [], text
+    fields = list(res[0][1]._fields)
+    keys = np.array([k for k, _ in res], dtype=np.int64)
+    vals = np.array([[float(getattr(t, f)) for f in fields] for _, t in res])
+    o = np.argsort(keys, kind="stable")
+    return keys[o], vals[o], fields, text
+
+
+def save(name, pid, pk, value, cfg, public=None, **extra):
+    keys, vals, fields, text = run_reference(pid, pk, value, cfg, public)
+    np.savez_compressed(
+        os.path.join(OUT, name + ".npz"),
+        pid=np.asarray(pid if pid is not None else [], dtype=np.int64),
+        pk=np.asarray(pk, dtype=np.int64),
+        value=np.asarray(value if value is not None else [], dtype=np.float64),
+        public=np.asarray(public if public is not None else [], dtype=np.int64),
+        has_public=np.asarray(public is not None),
+        out_keys=keys, out_vals=vals,
+        meta=np.asarray(json.dumps(dict(cfg=cfg, fields=fields, report=text, **extra))))
+    print(f"{name}: {len(pk)} rows -> {len(keys)} partitions, fields={fields}")
+
+
+def nonbinding(pid, pk):
+    pairs = {}
+    per_pid = {}
+    for a, b in zip(pid.tolist(), pk.tolist()):
+        pairs[(a, b)] = pairs.get((a, b), 0) + 1
+        per_pid.setdefault(a, set()).add(b)
+    return max(len(s) for s in per_pid.values()), max(pairs.values())
+
+
+def netflix():
+    """contributing/sample_combined_data_1.txt in Netflix format, parsed like
+    examples/movie_view_ratings/common_utils.py:51-59 (movie_id line ends
+    with ':', then 'user_id,rating,date')."""
+    movie, users, movies, ratings = None, [], [], []
+    with open(os.path.join(REF, "contributing", "sample_combined_data_1.txt")) as f:
+        for line in f:
+            line = line.strip()
+            if not line:
+                continue
+            if line[-1] == ":":
+                movie = int(line[:-1])
+            else:
+                u, r, _ = line.split(",")
+                users.append(int(u))
+                movies.append(movie)
+                ratings.append(float(r))
+    return np.array(users), np.array(movies), np.array(ratings)
+
+
+def main():
+    os.makedirs(OUT, exist_ok=True)
+    rng = np.random.default_rng(20250204)
+
+    # A. Netflix sample, configs[0] shape: COUNT+SUM+MEAN(+PID count).
+    u, m, r = netflix()
+    L0, Linf = nonbinding(u, m)
+    save("netflix_count_sum_mean", u, m, r,
+         dict(metrics=["count", "sum", "mean", "privacy_id_count"], L0=L0, Linf=Linf,
+              min_value=1.0, max_value=5.0))
+
+    # Synthetic data with clipping active (values outside [a, b]).
+    n, U, P = 20000, 400, 250
+    pid = rng.integers(0, U, n)
+    pk = np.minimum(rng.zipf(1.3, n) - 1, P - 1)
+    val = rng.normal(5.0, 3.0, n)
+    L0, Linf = nonbinding(pid, pk)
+    save("synth_count_sum_mean", pid, pk, val,
+         dict(metrics=["count", "sum", "mean"], L0=L0, Linf=Linf, min_value=0.0, max_value=10.0))
+    save("synth_variance", pid, pk, val,
+         dict(metrics=["variance", "mean", "count", "sum"], L0=L0, Linf=Linf,
+              min_value=-2.0, max_value=7.0, noise_kind="gaussian"))
+    save("synth_count_sum_pidcount", pid, pk, val,
+         dict(metrics=["count", "sum", "privacy_id_count"], L0=L0, Linf=Linf,
+              min_value=1.0, max_value=8.0))
+    save("synth_per_partition_sum", pid, pk, val,
+         dict(metrics=["count", "sum"], L0=L0, Linf=Linf,
+              min_sum_per_partition=-5.0, max_sum_per_partition=40.0))
+    save("synth_mean_min_eq_max", pid, pk, val,
+         dict(metrics=["mean", "count"], L0=L0, Linf=Linf, min_value=3.0, max_value=3.0))
+    save("synth_count_only", pid, pk, None,
+         dict(metrics=["count", "privacy_id_count"], L0=L0, Linf=Linf))
+
+    # Public partitions: a subset of observed keys plus absent ones.
+    public = sorted(set(range(0, P, 3)) | {P + 5, P + 17})
+    save("synth_public_partitions", pid, pk, val,
+         dict(metrics=["count", "sum", "privacy_id_count"], L0=L0, Linf=Linf,
+              min_value=0.0, max_value=10.0, noise_kind="gaussian"), public=public)
+    save("synth_public_mean_empty", pid, pk, val,
+         dict(metrics=["mean", "count", "sum"], L0=L0, Linf=Linf,
+              min_value=-1.0, max_value=4.0), public=public)
+
+    # contribution_bounds_already_enforced (no privacy ids).
+    save("synth_already_enforced_public", None, pk, val,
+         dict(metrics=["count", "sum"], L0=3, Linf=2, min_value=0.0, max_value=10.0,
+              already_enforced=True), public=public)
+    save("synth_already_enforced_private", None, pk, val,
+         dict(metrics=["sum"], L0=3, Linf=2, min_value=0.0, max_value=10.0,
+              already_enforced=True))
+
+    # Binding bounds: mean over reference runs (distributional target).
+    nb, Ub, Pb = 600, 30, 12
+    pidb = rng.integers(0, Ub, nb)
+    pkb = rng.integers(0, Pb, nb)
+    valb = rng.uniform(0, 10, nb)
+    cfg = dict(metrics=["count", "sum", "privacy_id_count"], L0=3, Linf=2,
+               min_value=0.0, max_value=10.0)
+    runs = 400
+    acc = []
+    for s in range(runs):
+        keys, vals, fields, _ = run_reference(pidb, pkb, valb, cfg, seed=s)
+        full = np.zeros((Pb, len(fields)))
+        full[keys] = vals
+        acc.append(full)
+    acc = np.array(acc)
+    np.savez_compressed(os.path.join(OUT, "binding_count_sum_pidcount.npz"),
+                        pid=pidb, pk=pkb, value=valb, runs=runs,
+                        mean=acc.mean(0), std=acc.std(0),
+                        meta=np.asarray(json.dumps(dict(cfg=cfg, fields=fields))))
+    print(f"binding: {runs} runs, fields={fields}")
+
+
+if __name__ == "__main__":
+    main()

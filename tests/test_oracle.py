@@ -1,0 +1,157 @@
+"""Pins the CPU oracle (oracle/pdp_oracle.py) against the reference:
+golden vectors produced by the reference LocalBackend (oracle/gen_golden.py)
+and the known-answer numbers of the reference's own tests."""
+import math
+
+import numpy as np
+import pytest
+from scipy.stats import binom
+
+import pdp_oracle as o
+from golden_util import aggregate_cases, encode_case, known_answers, load, sum_tolerance
+
+
+def oracle_run(d, sampler="feistel", seed=0, noise=False):
+    cfg = d["meta"]["cfg"]
+    pid, pk, keys = encode_case(d)
+    value = d["value"] if len(d["value"]) else None
+    bp = o.BoundParams(cfg["L0"], cfg["Linf"], cfg.get("min_value"), cfg.get("max_value"),
+                       cfg.get("min_sum_per_partition"), cfg.get("max_sum_per_partition"),
+                       cfg.get("already_enforced", False))
+    acc = o.bound_and_accumulate(pid, pk, value, len(keys), bp, sampler=sampler, seed=seed)
+    metrics = tuple(cfg["metrics"])
+    budgets = {m: (0.5, 1e-7) for m in ("count", "sum", "mean", "variance", "privacy_id_count")}
+    public = bool(d["has_public"])
+    spec = o.ReleaseSpec(metrics, cfg.get("noise_kind", "laplace"), budgets,
+                         None if public else "truncated_geometric", (0.5, 1e-7),
+                         cfg["Linf"] if cfg.get("already_enforced") else 1)
+    keep, out = o.release(acc, bp, spec, seed=seed, noise=noise)
+    return keys, keep, out, acc
+
+
+@pytest.mark.parametrize("name", aggregate_cases())
+def test_oracle_matches_reference_golden(name):
+    d = load(name)
+    keys, keep, out, acc = oracle_run(d)
+    fields = d["meta"]["fields"]
+    assert fields == o.metric_field_order(d["meta"]["cfg"]["metrics"])
+    np.testing.assert_array_equal(keys[keep], d["out_keys"])
+    vals = d["out_vals"]
+    # scale for float tolerance: sum of |values| bounded by count * max|v|
+    vmax = float(np.abs(d["value"]).max()) if len(d["value"]) else 1.0
+    for j, f in enumerate(fields):
+        got = out[f][keep]
+        exp = vals[:, j]
+        if f in ("count", "privacy_id_count"):
+            np.testing.assert_array_equal(got, exp)
+        else:
+            scale = (acc.count[keep] + 1) * max(vmax, 1.0)**2
+            assert np.all(np.abs(got - exp) <= sum_tolerance(exp, scale)), f
+
+
+def test_gaussian_sigma_known_answers():
+    for c in known_answers()["gaussian_sigma"]:
+        l2 = c["l2"] if "l2" in c else math.sqrt(c["l0"]) * c["linf"]
+        assert o.gaussian_sigma(c["eps"], c["delta"], l2) == pytest.approx(c["sigma"], abs=1e-12), c
+
+
+def test_truncated_geometric_known_answers():
+    for c in known_answers()["truncated_geometric"]:
+        n, p = c["n_binomial"]
+        ks = np.arange(n + 1)
+        pm = binom.pmf(ks, n, p)
+        got = float((pm * o.truncated_geometric_keep_prob(ks, c["eps"], c["delta"], c["k"])).sum())
+        assert got == pytest.approx(c["p_keep"], abs=1e-10), c
+
+
+def test_laplace_std_known_answers():
+    for c in known_answers()["laplace_std"]:
+        if "std" in c:
+            linf = max(abs(c["min_sum"]), abs(c["max_sum"]))
+            assert o.noise_scale("laplace", c["eps"], 0, c["l0"], linf) * math.sqrt(2) == pytest.approx(c["std"], abs=1e-10)
+        else:
+            assert o.noise_scale("laplace", c["eps"], 0, c["l0"], c["linf"]) * math.sqrt(2) == pytest.approx(
+                c["l0"] * c["linf"] / c["eps"] * math.sqrt(2), abs=1e-10)
+
+
+def test_equally_split_budget_known_answer():
+    c = known_answers()["equally_split_budget"]
+    exp = [(0.5 / 5, 1e-10 / 5) for _ in range(4)] + [(0.5 - 4 * (0.5 / 5), 1e-10 - 4 * (1e-10 / 5))]
+    assert o.equally_split_budget(c["eps"], c["delta"], c["n"]) == exp
+    with pytest.raises(ValueError):
+        o.equally_split_budget(0.5, 1e-10, 0)
+
+
+def test_bounder_known_answer():
+    # contribution_bounders_test.py:60-69: (2, 7, 25) / (2, 3, 5) -> with an
+    # accumulator of (len, sum, sum of squares) on values 1..4.
+    pid = np.array([0, 0, 0, 0])
+    pk = np.array([0, 0, 1, 1])
+    v = np.array([1.0, 2.0, 3.0, 4.0])
+    acc = o.bound_and_accumulate(pid, pk, v, 2, o.BoundParams(2, 2, -100.0, 100.0))
+    mid = 0.0
+    np.testing.assert_array_equal(acc.count, [2, 2])
+    np.testing.assert_allclose(acc.sum, [3, 7])
+    np.testing.assert_allclose(acc.nsumsq, [5, 25])
+    assert mid == o.compute_middle(-100.0, 100.0)
+
+
+def test_accumulator_known_answers():
+    # combiners_test.py:337-341 mean acc [1,3] with [0,4] -> (2, 0)
+    acc = o.bound_and_accumulate(np.zeros(2), np.zeros(2), np.array([1.0, 3.0]), 1,
+                                 o.BoundParams(1, 5, 0.0, 4.0))
+    assert (acc.count[0], acc.nsum[0]) == (2, 0.0)
+    # combiners_test.py:391-395 variance acc [1,2] -> (2, -1, 1)
+    acc = o.bound_and_accumulate(np.zeros(2), np.zeros(2), np.array([1.0, 2.0]), 1,
+                                 o.BoundParams(1, 5, 0.0, 4.0))
+    assert (acc.count[0], acc.nsum[0], acc.nsumsq[0]) == (2, -1.0, 1.0)
+    # combiners_test.py:275-282 per-partition sum clipping [0, 3]
+    for vals, exp in ([2, 0.5], 2.5), ([4, 1], 3), ([-10, 5, 3], 0):
+        acc = o.bound_and_accumulate(np.zeros(len(vals)), np.zeros(len(vals)), np.array(vals, float), 1,
+                                     o.BoundParams(1, 10, None, None, 0.0, 3.0))
+        assert acc.sum[0] == exp
+    # combiners_test.py:405-412 variance no-noise (4, 0, 2) with [0, 4]
+    a = o.Accumulators(np.array([1]), np.array([4]), np.array([8.0]), np.array([0.0]), np.array([2.0]))
+    keep, out = o.release(a, o.BoundParams(1, 1, 0.0, 4.0),
+                          o.ReleaseSpec(("variance", "mean", "count", "sum"), "laplace",
+                                        {"variance": (1.0, 0.0)}), noise=False)
+    assert (out["count"][0], out["sum"][0], out["mean"][0], out["variance"][0]) == (4, 8, 2, 0.5)
+
+
+def test_feistel_is_bijection():
+    for bits in (1, 2, 5, 8, 13, 20):
+        x = np.arange(1 << bits, dtype=np.uint64)
+        y = o.perm_bits(x, bits, np.uint64(12345))
+        assert len(np.unique(y)) == len(x) and y.max() < (1 << bits)
+    for n in (2, 3, 7, 100, 1000):
+        y = o.cycle_walk(np.arange(n), np.full(n, n), np.full(n, 99, dtype=np.uint64))
+        assert sorted(y.tolist()) == list(range(n))
+
+
+def test_feistel_sampler_is_uniform():
+    """Inclusion frequency of each row under L_inf sampling ~ L_inf/n."""
+    n, linf, trials = 7, 3, 4000
+    hits = np.zeros(n)
+    for s in range(trials):
+        y = o.cycle_walk(np.arange(n), np.full(n, n), np.full(n, o.group_perm_key(s, 1, 2), dtype=np.uint64))
+        hits += y < linf
+    p = linf / n
+    tol = 4 * math.sqrt(p * (1 - p) / trials)
+    assert np.all(np.abs(hits / trials - p) < tol)
+
+
+def test_binding_bounds_match_reference_distribution():
+    """oracle feistel sampler vs mean of 400 reference LocalBackend runs."""
+    d = load("binding_count_sum_pidcount")
+    cfg = d["meta"]["cfg"]
+    P = d["mean"].shape[0]
+    bp = o.BoundParams(cfg["L0"], cfg["Linf"], cfg["min_value"], cfg["max_value"])
+    runs = 400
+    res = np.zeros((runs, P, 3))
+    for s in range(runs):
+        acc = o.bound_and_accumulate(d["pid"], d["pk"], d["value"], P, bp, "feistel", seed=1000 + s)
+        res[s] = np.stack([acc.count, acc.sum, acc.row_count], 1)
+    ref_mean, ref_std = d["mean"], d["std"]
+    se = np.sqrt(ref_std**2 / int(d["runs"]) + res.std(0)**2 / runs) + 1e-9
+    z = np.abs(res.mean(0) - ref_mean) / se
+    assert z.max() < 5.0, z.max()
