@@ -1,0 +1,189 @@
+"""Benchmark: DP COUNT+SUM+MEAN with contribution bounding and private partition
+selection (BASELINE.json metric) on synthetic Zipf(1.1)-keyed rows.
+
+  python bench.py [--gpus N --steps K --warmup W]
+
+One "step" = one pass of the hot path over one batch: pdp_bound_accumulate
+(histogram + radix passes + LDS bucket bounding/accumulation) [+ RCCL
+reduce-scatter of the per-partition accumulators when N > 1] + pdp_release
+(truncated-geometric selection + Laplace noise).  Inputs (int64 pid, int64
+pk, f64 value) are generated on device before timing and stay resident.
+Weak scaling: every rank processes --rows rows of its own privacy ids.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=5)
+    p.add_argument("--warmup", type=int, default=2)
+    p.add_argument("--rows", type=float, default=1e9, help="rows per GPU")
+    p.add_argument("--partitions", type=float, default=1e6)
+    p.add_argument("--pids", type=float, default=1e7, help="privacy ids per GPU")
+    p.add_argument("--zipf", type=float, default=1.1)
+    p.add_argument("--l0", type=int, default=4)
+    p.add_argument("--linf", type=int, default=2)
+    p.add_argument("--cpu-sample", type=float, default=12e6, help="rows of the CPU baseline sample")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-profile", action="store_true")
+    p.add_argument("--seed", type=int, default=20250204)
+    return p.parse_args()
+
+
+def stage_bytes(stage, n_in, n_kept, P, nfields):
+    """Algorithmic bytes of one launch of each kernel (Roofline)."""
+    return {
+        "histogram": 16 * n_in,  # read int64 pid + int64 pk
+        "onesweep_first": (24 + 16) * n_in,  # read 3 columns, write 16-B records
+        "onesweep_rest": 32 * n_kept,  # read + write 16-B records
+        "buckets": 16 * n_kept,  # read 16-B records once
+        "release": P * (3 * 8 + 1 + 8 * nfields),
+    }.get(stage)
+
+
+def cpu_baseline(args, P):
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pdp_oracle as o  # checker / baseline only
+    m = int(args.cpu_sample)
+    U = max(1, int(args.pids * m / args.rows))
+    pid, pk, val = o.synth_rows(m, U, P, seed=args.seed, zipf_s=args.zipf)
+    bp = o.BoundParams(args.l0, args.linf, 0.0, 10.0)
+    spec = o.ReleaseSpec(("mean", "count", "sum"), "laplace", {"mean": (0.5, 0.0)}, "truncated_geometric",
+                         (0.5, 1e-6))
+    t0 = time.perf_counter()
+    acc = o.bound_and_accumulate(pid, pk, val, P, bp, "feistel", seed=1)
+    o.release(acc, bp, spec, seed=2)
+    dt = time.perf_counter() - t0
+    return {"value": m / dt, "unit": "rows/s", "cores": 1, "kind": "port",
+            "sample": f"{m} rows, {U} privacy ids, {P} Zipf({args.zipf}) partitions; numpy oracle "
+                      f"(oracle/pdp_oracle.py) on 1 host core, {dt:.1f} s"}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    from pipelinedp_amd import native
+    from pipelinedp_amd.distributed import World
+    from pipelinedp_amd.executor import BoundConfig, HipExecutor, ReleaseConfig
+
+    world_size = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    world = None
+    if world_size > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        world = World(rank, world_size)
+
+    n = int(args.rows)
+    P = int(args.partitions)
+    U = int(args.pids)
+    ex = HipExecutor(local)
+    pid, pk, val = ex.generate(n, U, P, seed=args.seed, zipf_s=args.zipf, lo=0.0, hi=10.0, row_offset=rank * n)
+    mask = native.METRIC_COUNT | native.METRIC_SUM | native.METRIC_MEAN
+    bounds = BoundConfig(mask, args.l0, args.linf, 0.0, 10.0, sampling_seed=args.seed + 1)
+    # NaiveBudgetAccountant(eps=1, delta=1e-6): MeanCombiner (Laplace) eps 0.5, selection eps 0.5 delta 1e-6
+    eps = [0.0] * 6
+    delta = [0.0] * 6
+    eps[native.MECH_MEAN] = 0.5
+    eps[native.MECH_SELECTION], delta[native.MECH_SELECTION] = 0.5, 1e-6
+    rel = ReleaseConfig(mask, native.NOISE_LAPLACE, native.SELECTION_TRUNCATED_GEOMETRIC, eps, delta, 1, True,
+                        noise_seed=args.seed + 2)
+    fields = native.metric_fields(mask)
+
+    def step():
+        if world is not None:
+            return world.aggregate(ex, pid, pk, val, U, P, bounds, rel, gather=False)
+        acc = ex.accumulate(pid, pk, val, U, P, bounds)
+        return ex.release(acc, rel, bounds)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    st = ex.stats()
+    kept_rows = int(st.kept_rows_in)
+    if not args.no_profile:
+        ex.profile(True)
+        ex.profile_read(reset=True)
+    if world is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        res = step()
+    torch.cuda.synchronize()
+    if world is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world is not None:
+        t = torch.tensor([elapsed], device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    kept_parts = int(res[0].sum().item())
+
+    roofline = None
+    stages = {}
+    if not args.no_profile:
+        prof = ex.profile_read(reset=True)
+        ex.profile(False)
+        for s, (ms, cnt) in prof.items():
+            if cnt:
+                stages[s] = {"ms_per_launch": ms / cnt, "launches_per_step": cnt / args.steps}
+        dom = max(stages, key=lambda s: stages[s]["ms_per_launch"] * stages[s]["launches_per_step"])
+        nb = (P + world_size - 1) // world_size if world else P
+        b = stage_bytes(dom, n, kept_rows, nb, len(fields))
+        ach = b / (stages[dom]["ms_per_launch"] * 1e-3) / 1e9
+        traffic = None
+        pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+        if os.path.exists(pmc_path):
+            pmc = json.load(open(pmc_path))
+            if pmc.get("config_rows") == n and dom in pmc.get("bytes_per_launch", {}):
+                traffic = pmc["bytes_per_launch"][dom]
+        roofline = {"bound": "hbm", "kernel": dom, "achieved": round(ach, 1), "peak": PEAK_HBM_GBS,
+                    "unit": "GB/s", "frac": round(ach / PEAK_HBM_GBS, 4), "traffic": traffic,
+                    "algorithmic_bytes_per_launch": b}
+        for s in stages:
+            bs = stage_bytes(s, n, kept_rows, nb, len(fields))
+            if bs:
+                stages[s]["achieved_GBs"] = round(bs / (stages[s]["ms_per_launch"] * 1e-3) / 1e9, 1)
+
+    rows_per_s = n * world_size * args.steps / elapsed
+    cpu = None
+    if rank == 0 and world_size == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args, P)
+    if rank == 0:
+        line = {
+            "metric": "input rows/sec (node) for DP COUNT+SUM+MEAN, 1B rows/1M partitions; % HBM peak",
+            "value": rows_per_s, "unit": "rows/s", "n_gpus": world_size, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic (on-device Philox generator, oracle/pdp_oracle.py:synth_rows)",
+            "config": {"workload": f"DP COUNT+SUM+MEAN, {n:.2e} rows/GPU, {U:.1e} privacy ids/GPU, "
+                                   f"{P:.1e} Zipf({args.zipf}) partitions, L0={args.l0}, Linf={args.linf}, "
+                                   f"[0,10], Laplace, truncated-geometric selection, eps=1 delta=1e-6",
+                       "rows_per_gpu": n, "partitions": P, "privacy_ids_per_gpu": U,
+                       "parallelism": f"pid-sharded x{world_size}" + (" + RCCL reduce-scatter" if world else "")},
+            "roofline": roofline, "cpu_baseline": cpu,
+            "kernels": stages, "kept_rows": kept_rows, "kept_partitions_rank0": kept_parts,
+            "sort_passes": int(st.sort_passes), "bucket_low_bits": int(st.bucket_low_bits),
+            "fallback_rows": int(st.fallback_rows),
+        }
+        print(json.dumps(line), flush=True)
+    if world is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

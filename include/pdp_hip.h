@@ -1,0 +1,225 @@
+/*
+ * pdp_hip.h — C ABI of libpdp_hip.so, the MI355X (gfx950) implementation of
+ * PipelineDP's DPEngine.aggregate hot path.
+ *
+ * Reference interfaces replaced (paths under /root/reference):
+ *   pdp_bound_accumulate   <- SamplingCrossAndPerPartitionContributionBounder
+ *                             .bound_contributions (pipeline_dp/contribution_bounders.py:66-105)
+ *                             + CompoundCombiner.create_accumulator/merge_accumulators
+ *                             (pipeline_dp/combiners.py:558-573)
+ *                             + LocalBackend.combine_accumulators_per_key
+ *                             (pipeline_dp/pipeline_backend.py:528-538)
+ *                             + the contribution_bounds_already_enforced branch
+ *                             (pipeline_dp/dp_engine.py:139-150)
+ *                             + _drop_not_public_partitions / _add_empty_public_partitions
+ *                             (pipeline_dp/dp_engine.py:283-310): pk < 0 rows are dropped,
+ *                             every partition in [0, num_partitions) gets an accumulator.
+ *   pdp_release            <- DPEngine._select_private_partitions_internal
+ *                             (pipeline_dp/dp_engine.py:312-362) + partition_selection.py:19-33
+ *                             + CompoundCombiner.compute_metrics (combiners.py:575-597)
+ *                             -> dp_computations.compute_dp_count/sum/mean/var
+ *                             (pipeline_dp/dp_computations.py:255-459)
+ *   pdp_gaussian_sigma     <- dp_computations.compute_sigma (dp_computations.py:98-108; PyDP)
+ *   pdp_truncated_geometric_table / pdp_selection_threshold
+ *                          <- PyDP partition-selection strategies (partition_selection.py:24-33)
+ *   pdp_metric_fields      <- MetricsTuple field order (combiners.py:575-597, 652-720)
+ *
+ * Conventions: every pointer in the column/accumulator/output structs is a
+ * DEVICE pointer owned by the caller; `stream` is a hipStream_t (NULL = null
+ * stream).  The library allocates nothing on the hot path except a rarely
+ * used fallback (overflowing privacy-id buckets).  Functions return 0 on
+ * success and a negative PDP_ERR_* code on failure; pdp_last_error() gives a
+ * thread-local message.  No exceptions cross the ABI.
+ */
+#ifndef PDP_HIP_H_
+#define PDP_HIP_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PDP_ABI_VERSION 1
+
+enum {
+  PDP_OK = 0,
+  PDP_ERR_INVALID_ARG = -1,
+  PDP_ERR_HIP = -2,
+  PDP_ERR_WORKSPACE = -3,
+  PDP_ERR_OUT_OF_RANGE = -4,
+  PDP_ERR_INTERNAL = -5,
+};
+
+/* Metric bitmask (aggregate_params.py:54-65). */
+enum {
+  PDP_METRIC_COUNT = 1,
+  PDP_METRIC_SUM = 2,
+  PDP_METRIC_MEAN = 4,
+  PDP_METRIC_VARIANCE = 8,
+  PDP_METRIC_PRIVACY_ID_COUNT = 16,
+};
+
+/* Output field ids, in MetricsTuple naming. */
+enum {
+  PDP_FIELD_VARIANCE = 0,
+  PDP_FIELD_MEAN = 1,
+  PDP_FIELD_COUNT = 2,
+  PDP_FIELD_SUM = 3,
+  PDP_FIELD_PRIVACY_ID_COUNT = 4,
+};
+
+enum { PDP_NOISE_LAPLACE = 0, PDP_NOISE_GAUSSIAN = 1 }; /* aggregate_params.py:68-76 */
+
+enum { /* aggregate_params.py:92-95; NONE = public partitions */
+  PDP_SELECTION_NONE = 0,
+  PDP_SELECTION_TRUNCATED_GEOMETRIC = 1,
+  PDP_SELECTION_LAPLACE_THRESHOLDING = 2,
+  PDP_SELECTION_GAUSSIAN_THRESHOLDING = 3,
+};
+
+/* Budget slots (one MechanismSpec each, combiners.py:652-720, dp_engine.py:328). */
+enum {
+  PDP_MECH_COUNT = 0,
+  PDP_MECH_SUM = 1,
+  PDP_MECH_MEAN = 2,
+  PDP_MECH_VARIANCE = 3,
+  PDP_MECH_PRIVACY_ID_COUNT = 4,
+  PDP_MECH_SELECTION = 5,
+  PDP_NUM_MECH = 6,
+};
+
+/* Dictionary-encoded input columns (device).  pid in [0, num_privacy_ids),
+ * pk in [0, num_partitions); pk < 0 marks a row of a non-public partition
+ * (dropped).  value may be NULL for COUNT / PRIVACY_ID_COUNT only; pid may be
+ * NULL when bounds_already_enforced. */
+typedef struct pdp_columns {
+  const int64_t* pid;
+  const int64_t* pk;
+  const double* value;
+  int64_t num_rows;
+  int64_t num_privacy_ids;
+  int64_t num_partitions;
+} pdp_columns;
+
+/* AggregateParams subset that drives bounding (aggregate_params.py:98-296). */
+typedef struct pdp_bound_params {
+  int32_t metrics;                          /* PDP_METRIC_* mask */
+  int32_t bounds_already_enforced;          /* contribution_bounds_already_enforced */
+  int64_t max_partitions_contributed;       /* L0 */
+  int64_t max_contributions_per_partition;  /* L_inf */
+  int32_t has_value_bounds;                 /* min_value/max_value set */
+  int32_t has_partition_bounds;             /* min/max_sum_per_partition set */
+  double min_value, max_value;
+  double min_sum_per_partition, max_sum_per_partition;
+  uint64_t sampling_seed;                   /* keys the uniform sampling permutations */
+  int32_t debug_force_fallback;             /* testing: route every bucket through the
+                                               generic sorted-stream path */
+  int32_t reserved;
+} pdp_bound_params;
+
+/* Dense per-partition accumulators [num_partitions] (device).  row_count is the
+ * CompoundCombiner row count (= privacy-id count; rows when bounds already
+ * enforced).  x = nsum (MEAN/VARIANCE: sum of clip(v)-middle) or sum (SUM only:
+ * sum of clip(v), or of per-(pid,pk) clipped sums); y = nsumsq (VARIANCE). */
+typedef struct pdp_accumulators {
+  int64_t* row_count;
+  int64_t* count;
+  double* x;
+  double* y;
+} pdp_accumulators;
+
+typedef struct pdp_release_params {
+  int32_t metrics;
+  int32_t noise_kind;
+  int32_t selection;
+  int32_t add_noise;                 /* 0 = noise-free (explain / testing) */
+  int64_t max_partitions_contributed;
+  int64_t max_contributions_per_partition;
+  int32_t has_value_bounds;
+  int32_t has_partition_bounds;
+  double min_value, max_value;
+  double min_sum_per_partition, max_sum_per_partition;
+  double eps[PDP_NUM_MECH];
+  double delta[PDP_NUM_MECH];
+  int64_t max_rows_per_privacy_id;   /* dp_engine.py:163-169 */
+  uint64_t noise_seed;
+} pdp_release_params;
+
+typedef struct pdp_outputs {
+  uint8_t* keep;    /* [num_partitions] 1 = partition released */
+  double* metrics;  /* [num_fields][num_partitions], order from pdp_metric_fields */
+} pdp_outputs;
+
+typedef struct pdp_ctx pdp_ctx;
+
+int pdp_abi_version(void);
+const char* pdp_last_error(void);
+
+pdp_ctx* pdp_ctx_create(int device);
+void pdp_ctx_destroy(pdp_ctx* ctx);
+
+/* Bytes of device workspace pdp_bound_accumulate needs for these columns. */
+int pdp_workspace_size(const pdp_columns* cols, const pdp_bound_params* bp, size_t* bytes);
+
+/* Rows -> dense per-partition accumulators (zeroed first). */
+int pdp_bound_accumulate(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp,
+                         const pdp_accumulators* acc, void* workspace, size_t workspace_bytes,
+                         void* stream);
+
+/* Accumulators of partitions [pk_offset, pk_offset + num_partitions) ->
+ * selection + noisy metrics.  Philox counters use the global partition id
+ * (pk_offset + i), so the result does not depend on how partitions are
+ * distributed over ranks. */
+int pdp_release(pdp_ctx* ctx, const pdp_accumulators* acc, int64_t num_partitions, int64_t pk_offset,
+                const pdp_release_params* rp, const pdp_outputs* out, void* stream);
+
+/* Field order of MetricsTuple for a metric mask; returns the count. */
+int pdp_metric_fields(int32_t metrics, int32_t* fields_out /* >= 5 */);
+
+/* Host-side calibration (no GPU needed). */
+double pdp_gaussian_sigma(double eps, double delta, double l2_sensitivity);
+int pdp_truncated_geometric_table(double eps, double delta, int64_t max_partitions, double* out,
+                                  int64_t capacity, int64_t* length);
+int pdp_selection_threshold(int32_t selection, double eps, double delta, int64_t max_partitions,
+                            double* threshold, double* scale);
+
+/* Synthetic workload (bench / tests): rows [row_offset, row_offset+n) of the
+ * generator specified in oracle/pdp_oracle.py:synth_rows. */
+int pdp_generate_synthetic(int64_t* pid, int64_t* pk, double* value, int64_t n, int64_t row_offset,
+                           int64_t num_privacy_ids, int64_t num_partitions, double zipf_s,
+                           int32_t value_kind, double value_lo, double value_hi, uint64_t seed,
+                           void* stream);
+
+/* Statistics of the last pdp_bound_accumulate on this ctx (host values). */
+typedef struct pdp_stats {
+  int64_t kept_rows_in;        /* rows after dropping non-public partitions */
+  int64_t fallback_rows;       /* rows routed through the generic path */
+  int64_t fallback_ranges;
+  int32_t sort_passes;
+  int32_t bucket_low_bits;
+} pdp_stats;
+int pdp_get_stats(pdp_ctx* ctx, pdp_stats* out);
+
+/* Per-stage device timing with hipEvents recorded on the launch stream (for
+ * bench.py's roofline).  Stages: */
+enum {
+  PDP_STAGE_HISTOGRAM = 0,       /* K0 */
+  PDP_STAGE_ONESWEEP_FIRST = 1,  /* K1 pass 0 (reads the int64/int64/f64 columns) */
+  PDP_STAGE_ONESWEEP_REST = 2,   /* K1 passes >= 1 */
+  PDP_STAGE_BUCKETS = 3,         /* K2 */
+  PDP_STAGE_GENERIC = 4,         /* KF (fallback) */
+  PDP_STAGE_RELEASE = 5,         /* K5/K6 */
+  PDP_STAGE_ENFORCED = 6,        /* bounds already enforced accumulate */
+  PDP_NUM_STAGES = 7,
+};
+int pdp_profile_enable(pdp_ctx* ctx, int enable);
+/* Waits for recorded events; adds into ms_out/launches_out[PDP_NUM_STAGES]
+ * the totals since the last reset. */
+int pdp_profile_read(pdp_ctx* ctx, double* ms_out, int64_t* launches_out, int reset);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PDP_HIP_H_ */

@@ -1,0 +1,1709 @@
+// libpdp_hip.so — MI355X (gfx950) kernels for PipelineDP's DPEngine.aggregate
+// hot path.  C ABI in include/pdp_hip.h; design in DESIGN.md.
+//
+// Pipeline of pdp_bound_accumulate (main path):
+//   K0 k_histogram  : one read of pid/pk -> digit histograms of every radix
+//                     pass (+ count of dropped / invalid rows)
+//   K1 k_onesweep   : LSD radix passes on key = pid >> low (stable, decoupled
+//                     look-back); pass 0 packs the SoA int64/int64/f64 columns
+//                     into 16-byte records and drops non-public rows
+//   K2 k_buckets    : per workgroup, LDS batches of whole privacy-id buckets:
+//                     bitonic sort by (pid, pi_pid(pk), input order), L_inf and
+//                     L0 uniform sampling, clipping, per-(pid,pk) accumulators,
+//                     fp64/int64 atomics into the dense [P] partition
+//                     accumulators.  Buckets that do not fit LDS go to:
+//   KF generic path : LSD sort by (pid, pi_pid(pk)) + device-wide scans
+//                     (rare; exact same semantics).
+// pdp_release: K5/K6 k_release — selection + Laplace/Gaussian noise from
+// Philox, one thread per partition.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "pdp_hip.h"
+#include "pdp_rng.h"
+
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kItems = 16;                   // rows per thread in a radix tile
+constexpr int kTile = kThreads * kItems;     // 4096 rows per radix tile
+constexpr int kMaxPasses = 8;
+constexpr int kHist = 257;                   // 256 digits + drop bucket
+constexpr int kStatusStride = 256;
+constexpr int kSegCap = 2048;                // rows per LDS batch
+constexpr int kSegItems = kSegCap / kThreads;
+constexpr int kIdxBits = 11;                 // log2(kSegCap)
+constexpr int kBucketTarget = 768;           // expected rows per pid bucket
+constexpr unsigned kOverflowCap = 1u << 16;
+constexpr unsigned kNumCounters = 64;
+
+enum Counter {
+  kCtrInvalid = 0,
+  kCtrNKept = 1,
+  kCtrNRanges = 2,
+  kCtrFull = 3,
+  kCtrErr = 4,
+  kCtrNGeneric = 5,
+  kCtrTile0 = 16,  // 16..63 tile claim counters, one per onesweep launch
+};
+
+struct __align__(16) Rec {
+  uint32_t pid;
+  uint32_t pk;
+  double val;
+};
+
+struct KeySpec {
+  int mode;  // 0: key = pid >> low ; 1: key = (pid << pkb) | pi_pid(pk)
+  int passes;
+  int shift[kMaxPasses];
+  int bits[kMaxPasses];
+  int low;
+  int pkb;
+  uint64_t seed;
+  uint32_t num_pids;
+  uint32_t num_parts;
+};
+
+// How a row's value feeds the accumulators (combiners.py:254-261, 305-311,
+// 364-373).
+enum XMode { kXNone = 0, kXNsum = 1, kXClipSum = 2, kXRawSum = 3 };
+
+struct SegParams {
+  int low;
+  int pkb;
+  uint64_t seed;
+  int64_t l0;
+  int64_t linf;
+  int xmode;
+  int want_y;
+  int want_count;
+  int has_value;
+  double a, b, mid;
+  double smin, smax;
+};
+
+struct AccPtrs {
+  unsigned long long* row_count;
+  unsigned long long* count;
+  double* x;
+  double* y;
+};
+
+struct OvList {
+  unsigned long long* ranges;  // [cap][2] (start, end)
+  unsigned long long* counters;
+};
+
+__device__ __forceinline__ uint64_t sort_key(const KeySpec& ks, uint32_t pid, uint32_t pk) {
+  if (ks.mode == 0) return (uint64_t)(pid >> ks.low);
+  const uint32_t pi = pdp::perm_bits(pk, ks.pkb, pdp::pk_perm_key(ks.seed, pid));
+  return ((uint64_t)pid << ks.pkb) | pi;
+}
+
+__device__ __forceinline__ uint32_t digit_of(const KeySpec& ks, int pass, uint64_t key) {
+  return (uint32_t)((key >> ks.shift[pass]) & ((1ull << ks.bits[pass]) - 1ull));
+}
+
+__device__ __forceinline__ double clip(double v, double lo, double hi) {
+  // NaN-propagating like np.clip.
+  return v < lo ? lo : (v > hi ? hi : v);
+}
+
+// ---------------------------------------------------------------------------
+// Block-level helpers (256 threads = 4 waves of 64)
+// ---------------------------------------------------------------------------
+
+template <typename T>
+__device__ __forceinline__ T wave_incl_scan(T v) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    T x = __shfl_up(v, o);
+    if (lane >= o) v += x;
+  }
+  return v;
+}
+
+// Exclusive scan across the block; returns exclusive prefix, sets total.
+template <typename T>
+__device__ __forceinline__ T block_excl_scan(T v, T* s_tmp /*[4]*/, T& total) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  T inc = wave_incl_scan(v);
+  if (lane == 63) s_tmp[wave] = inc;
+  __syncthreads();
+  T add = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    const T s = s_tmp[w];
+    if (w < wave) add += s;
+    tot += s;
+  }
+  __syncthreads();
+  total = tot;
+  return add + inc - v;
+}
+
+template <typename T>
+__device__ __forceinline__ T block_min(T v, T* s_tmp) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    T x = __shfl_xor(v, o);
+    v = x < v ? x : v;
+  }
+  if (lane == 0) s_tmp[wave] = v;
+  __syncthreads();
+  T r = s_tmp[0];
+#pragma unroll
+  for (int w = 1; w < 4; ++w) r = s_tmp[w] < r ? s_tmp[w] : r;
+  __syncthreads();
+  return r;
+}
+
+template <typename T>
+__device__ __forceinline__ T block_max(T v, T* s_tmp) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    T x = __shfl_xor(v, o);
+    v = x > v ? x : v;
+  }
+  if (lane == 0) s_tmp[wave] = v;
+  __syncthreads();
+  T r = s_tmp[0];
+#pragma unroll
+  for (int w = 1; w < 4; ++w) r = s_tmp[w] > r ? s_tmp[w] : r;
+  __syncthreads();
+  return r;
+}
+
+// ---------------------------------------------------------------------------
+// K0: digit histograms of every pass from one read of the keys
+// ---------------------------------------------------------------------------
+
+template <bool SOA>
+__global__ __launch_bounds__(kThreads) void k_histogram(const int64_t* __restrict__ pid,
+                                                        const int64_t* __restrict__ pk,
+                                                        const Rec* __restrict__ rin, int64_t n,
+                                                        KeySpec ks, unsigned long long* __restrict__ hist,
+                                                        unsigned long long* __restrict__ counters) {
+  __shared__ unsigned int sh[kMaxPasses * kHist];
+  for (int i = threadIdx.x; i < kMaxPasses * kHist; i += kThreads) sh[i] = 0;
+  __syncthreads();
+  unsigned int invalid = 0;
+  const int64_t stride = (int64_t)gridDim.x * kThreads;
+  for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < n; i += stride) {
+    uint32_t p32, k32;
+    if (SOA) {
+      const int64_t a = pid[i], b = pk[i];
+      if (b < 0 || b >= (int64_t)ks.num_parts || a < 0 || a >= (int64_t)ks.num_pids) {
+        if (b >= 0) ++invalid;
+        atomicAdd(&sh[256], 1u);
+        continue;
+      }
+      p32 = (uint32_t)a;
+      k32 = (uint32_t)b;
+    } else {
+      const Rec r = rin[i];
+      p32 = r.pid;
+      k32 = r.pk;
+    }
+    const uint64_t key = sort_key(ks, p32, k32);
+    for (int p = 0; p < ks.passes; ++p) atomicAdd(&sh[p * kHist + digit_of(ks, p, key)], 1u);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < ks.passes * kHist; i += kThreads)
+    if (sh[i]) atomicAdd(&hist[i], (unsigned long long)sh[i]);
+  if (invalid) atomicAdd(&counters[kCtrInvalid], (unsigned long long)invalid);
+}
+
+// Bucket start offsets (exclusive scan of each pass histogram) and the number
+// of rows that survive pass 0.
+__global__ __launch_bounds__(kThreads) void k_offsets(const unsigned long long* __restrict__ hist,
+                                                      unsigned long long* __restrict__ off, int passes,
+                                                      int64_t n, unsigned long long* __restrict__ counters,
+                                                      int n_slot) {
+  __shared__ unsigned long long s_tmp[4];
+  for (int p = 0; p < passes; ++p) {
+    const unsigned long long v = hist[p * kHist + threadIdx.x];
+    unsigned long long tot;
+    const unsigned long long ex = block_excl_scan(v, s_tmp, tot);
+    off[p * kHist + threadIdx.x] = ex;
+  }
+  if (threadIdx.x == 0) counters[n_slot] = (unsigned long long)n - hist[256];
+}
+
+// ---------------------------------------------------------------------------
+// K1: one stable LSD radix pass, single sweep with decoupled look-back.
+// ---------------------------------------------------------------------------
+
+constexpr uint64_t kFlagAgg = 1ull << 46;
+constexpr uint64_t kFlagPre = 2ull << 46;
+constexpr uint64_t kFlagMask = 3ull << 46;
+constexpr uint64_t kValMask = (1ull << 46) - 1ull;
+
+template <bool SOA>
+__global__ __launch_bounds__(kThreads, 2) void k_onesweep(
+    const int64_t* __restrict__ pid, const int64_t* __restrict__ pk, const double* __restrict__ val,
+    const Rec* __restrict__ rin, Rec* __restrict__ rout, int64_t n_in,
+    const unsigned long long* __restrict__ counters_n, int n_slot, KeySpec ks, int pass,
+    const unsigned long long* __restrict__ off, unsigned long long* __restrict__ status, uint32_t epoch,
+    unsigned long long* __restrict__ counters, int tile_slot) {
+  __shared__ Rec s_rec[kTile];
+  __shared__ uint16_t s_dig[kTile];
+  __shared__ unsigned int s_cnt[4][kHist + 1];
+  __shared__ unsigned int s_dstart[256];
+  __shared__ long long s_gbase[256];
+  __shared__ unsigned int s_tmp[4];
+  __shared__ unsigned int s_tile;
+  __shared__ unsigned int s_total;
+
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  if (t == 0) s_tile = (unsigned int)atomicAdd(&counters[tile_slot], 1ull);
+  for (int i = t; i < 4 * (kHist + 1); i += kThreads) (&s_cnt[0][0])[i] = 0;
+  __syncthreads();
+  const int64_t tile = s_tile;
+  const int64_t n_eff = SOA ? n_in : (int64_t)counters_n[n_slot];
+  const int64_t tile_start = tile * kTile;
+  if (tile_start >= n_eff) return;
+  const int radix_bits = ks.bits[pass];
+  const int radix = 1 << radix_bits;
+
+  Rec r[kItems];
+  uint32_t dg[kItems];
+  uint32_t rk[kItems];
+  const int64_t base = tile_start + (int64_t)wave * (kItems * 64) + lane;
+#pragma unroll
+  for (int k = 0; k < kItems; ++k) {
+    const int64_t idx = base + k * 64;
+    uint32_t d = 257;  // ignore
+    if (idx < n_eff) {
+      if (SOA) {
+        const int64_t a = pid[idx], b = pk[idx];
+        r[k].pid = (uint32_t)a;
+        r[k].pk = (uint32_t)b;
+        r[k].val = val ? val[idx] : 0.0;
+        if (b < 0 || b >= (int64_t)ks.num_parts || a < 0 || a >= (int64_t)ks.num_pids)
+          d = 256;  // dropped
+        else
+          d = digit_of(ks, pass, sort_key(ks, r[k].pid, r[k].pk));
+      } else {
+        r[k] = rin[idx];
+        d = digit_of(ks, pass, sort_key(ks, r[k].pid, r[k].pk));
+      }
+    }
+    dg[k] = d;
+  }
+
+  // Wave-level multisplit ranking (stable: item order = wave, k, lane).
+  const uint64_t lt = (1ull << lane) - 1ull;
+#pragma unroll
+  for (int k = 0; k < kItems; ++k) {
+    const uint32_t d = dg[k];
+    uint64_t peers = ~0ull;
+#pragma unroll
+    for (int b = 0; b < 9; ++b) {
+      const bool bit = (d >> b) & 1u;
+      const uint64_t bb = __ballot(bit);
+      peers &= bit ? bb : ~bb;
+    }
+    const uint32_t before = __popcll(peers & lt);
+    const uint32_t c = __popcll(peers);
+    const uint32_t basec = s_cnt[wave][d];
+    __builtin_amdgcn_wave_barrier();
+    if (before == 0) s_cnt[wave][d] = basec + c;
+    __builtin_amdgcn_wave_barrier();
+    rk[k] = basec + before;
+  }
+  __syncthreads();
+
+  // Per-digit tile counts, per-wave exclusive offsets, digit starts.
+  unsigned int tcount = 0;
+  {
+    const unsigned int c0 = s_cnt[0][t], c1 = s_cnt[1][t], c2 = s_cnt[2][t], c3 = s_cnt[3][t];
+    tcount = c0 + c1 + c2 + c3;
+    __syncthreads();
+    s_cnt[0][t] = 0;
+    s_cnt[1][t] = c0;
+    s_cnt[2][t] = c0 + c1;
+    s_cnt[3][t] = c0 + c1 + c2;
+  }
+  unsigned int total;
+  const unsigned int dstart = block_excl_scan(tcount, s_tmp, total);
+  s_dstart[t] = dstart;
+  if (t == 0) s_total = total;
+
+  // Decoupled look-back per digit.
+  if (t < radix) {
+    unsigned long long* st = status + (size_t)tile * kStatusStride;
+    const uint64_t ep = (uint64_t)epoch << 48;
+    uint64_t excl = 0;
+    if (tile == 0) {
+      __hip_atomic_store(&st[t], ep | kFlagPre | (uint64_t)tcount, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      __hip_atomic_store(&st[t], ep | kFlagAgg | (uint64_t)tcount, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      int64_t j = tile - 1;
+      unsigned int spins = 0;
+      while (true) {
+        const uint64_t s = __hip_atomic_load(&status[(size_t)j * kStatusStride + t], __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
+        const uint64_t f = s & kFlagMask;
+        if ((s >> 48) == (uint64_t)epoch && f != 0) {
+          excl += s & kValMask;
+          if (f == kFlagPre) break;
+          --j;
+          continue;
+        }
+        if (++spins > (1u << 24)) {
+          atomicOr(&counters[kCtrErr], 1ull);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      __hip_atomic_store(&st[t], ep | kFlagPre | (excl + tcount), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    s_gbase[t] = (long long)off[t] + (long long)excl - (long long)dstart;
+  }
+  __syncthreads();
+
+  // Scatter into LDS in digit order, then write contiguous digit runs.
+#pragma unroll
+  for (int k = 0; k < kItems; ++k) {
+    const uint32_t d = dg[k];
+    if (d < 256) {
+      const uint32_t pos = s_dstart[d] + s_cnt[wave][d] + rk[k];
+      s_rec[pos] = r[k];
+      s_dig[pos] = (uint16_t)d;
+    }
+  }
+  __syncthreads();
+  const unsigned int tot = s_total;
+  for (unsigned int i = t; i < tot; i += kThreads) {
+    const uint32_t d = s_dig[i];
+    rout[s_gbase[d] + (long long)i] = s_rec[i];
+  }
+  (void)radix_bits;
+}
+
+// ---------------------------------------------------------------------------
+// K2: privacy-id buckets in LDS: bounding + per-(pid,pk) accumulation
+// ---------------------------------------------------------------------------
+
+__device__ __forceinline__ void record_overflow(const OvList& ov, int64_t s, int64_t e) {
+  const unsigned long long i = atomicAdd(&ov.counters[kCtrNRanges], 1ull);
+  if (i < kOverflowCap) {
+    ov.ranges[2 * i] = (unsigned long long)s;
+    ov.ranges[2 * i + 1] = (unsigned long long)e;
+  } else {
+    atomicOr(&ov.counters[kCtrFull], 1ull);
+  }
+}
+
+__device__ __forceinline__ void row_terms(const SegParams& sp, double v, double& x, double& y) {
+  x = 0.0;
+  y = 0.0;
+  if (sp.xmode == kXNsum) {
+    const double c = clip(v, sp.a, sp.b) - sp.mid;
+    x = c;
+    y = c * c;
+  } else if (sp.xmode == kXClipSum) {
+    x = clip(v, sp.a, sp.b);
+  } else if (sp.xmode == kXRawSum) {
+    x = v;
+  }
+}
+
+__device__ __forceinline__ void emit_group(const SegParams& sp, const AccPtrs& acc, uint32_t pk, uint32_t cnt,
+                                           double x, double y) {
+  atomicAdd(&acc.row_count[pk], 1ull);
+  if (sp.want_count) atomicAdd(&acc.count[pk], (unsigned long long)cnt);
+  if (sp.xmode != kXNone) {
+    if (sp.xmode == kXRawSum) x = clip(x, sp.smin, sp.smax);  // combiners.py:256-259
+    atomicAdd(&acc.x[pk], x);
+  }
+  if (sp.want_y) atomicAdd(&acc.y[pk], y);
+}
+
+struct BucketSmem {
+  uint64_t key[kSegCap];
+  double val[kSegCap];
+  double gx[kSegCap];
+  double gy[kSegCap];
+  uint32_t pk[kSegCap];
+  uint32_t gpk[kSegCap];
+  uint32_t gcnt[kSegCap];
+  uint16_t gpos[kSegCap + 1];
+  uint16_t pfirst[kSegCap];
+  uint8_t gkeep[kSegCap];
+  int64_t tmp64[4];
+  unsigned int tmp32[4];
+};
+
+__device__ __forceinline__ bool is_bucket_start(const Rec* __restrict__ recs, int64_t p, int64_t n, int low) {
+  if (p >= n) return true;
+  if (p == 0) return true;
+  return (recs[p].pid >> low) != (recs[p - 1].pid >> low);
+}
+
+// Process rows [bs, be) (whole buckets, be - bs <= kSegCap).
+__device__ void process_batch(const Rec* __restrict__ recs, int64_t bs, int64_t be, const SegParams& sp,
+                              const AccPtrs& acc, const OvList& ov, BucketSmem& sm) {
+  const int t = threadIdx.x;
+  const int m = (int)(be - bs);
+  const uint32_t pid_base = (recs[bs].pid >> sp.low) << sp.low;
+
+  uint32_t rel[kSegItems];
+  uint32_t pkv[kSegItems];
+  uint32_t maxrel = 0;
+#pragma unroll
+  for (int k = 0; k < kSegItems; ++k) {
+    const int i = t + k * kThreads;
+    rel[k] = 0;
+    pkv[k] = 0;
+    if (i < m) {
+      const Rec r = recs[bs + i];
+      rel[k] = r.pid - pid_base;
+      pkv[k] = r.pk;
+      sm.pk[i] = r.pk;
+      sm.val[i] = r.val;
+      maxrel = rel[k] > maxrel ? rel[k] : maxrel;
+    }
+  }
+  maxrel = block_max(maxrel, sm.tmp32);
+  const int abits = pdp::ceil_log2_u64((uint64_t)maxrel + 1ull);
+  if (abits + sp.pkb + kIdxBits > 64) {
+    if (t == 0) record_overflow(ov, bs, be);
+    __syncthreads();
+    return;
+  }
+  const int shift_p = sp.pkb + kIdxBits;
+  int m2 = 1;
+  while (m2 < m) m2 <<= 1;
+#pragma unroll
+  for (int k = 0; k < kSegItems; ++k) {
+    const int i = t + k * kThreads;
+    if (i < m) {
+      const uint32_t pid = pid_base + rel[k];
+      const uint32_t pi = pdp::perm_bits(pkv[k], sp.pkb, pdp::pk_perm_key(sp.seed, pid));
+      sm.key[i] = ((uint64_t)rel[k] << shift_p) | ((uint64_t)pi << kIdxBits) | (uint64_t)i;
+    } else if (i < m2) {
+      sm.key[i] = ~0ull;
+    }
+  }
+  __syncthreads();
+
+  // Bitonic sort of m2 keys.
+  for (int size = 2; size <= m2; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int c = t; c < (m2 >> 1); c += kThreads) {
+        const int i = 2 * stride * (c / stride) + (c % stride);
+        const int j = i + stride;
+        const bool asc = (i & size) == 0;
+        const uint64_t a = sm.key[i], b = sm.key[j];
+        if ((a > b) == asc) {
+          sm.key[i] = b;
+          sm.key[j] = a;
+        }
+      }
+      __syncthreads();
+    }
+  }
+
+  // Group (pid,pk) and pid structure over the sorted positions.
+  const int q0 = t * kSegItems;
+  uint64_t keys[kSegItems];
+  uint32_t gst_mask = 0, pst_mask = 0;
+  uint32_t cg = 0, cp = 0;
+#pragma unroll
+  for (int k = 0; k < kSegItems; ++k) {
+    const int q = q0 + k;
+    keys[k] = q < m ? sm.key[q] : ~0ull;
+    if (q < m) {
+      const uint64_t prev = q > 0 ? sm.key[q - 1] : 0ull;
+      const bool g = (q == 0) || ((keys[k] >> kIdxBits) != (prev >> kIdxBits));
+      const bool p = (q == 0) || ((keys[k] >> shift_p) != (prev >> shift_p));
+      gst_mask |= (uint32_t)g << k;
+      pst_mask |= (uint32_t)p << k;
+      cg += g;
+      cp += p;
+    }
+  }
+  unsigned int gtot, ptot;
+  const unsigned int gex = block_excl_scan(cg, sm.tmp32, gtot);
+  const unsigned int pex = block_excl_scan(cp, sm.tmp32, ptot);
+  {
+    unsigned int g = gex, p = pex;
+#pragma unroll
+    for (int k = 0; k < kSegItems; ++k) {
+      const int q = q0 + k;
+      if (q < m) {
+        if ((gst_mask >> k) & 1u) {
+          sm.gpos[g] = (uint16_t)q;
+          sm.gcnt[g] = 0;
+          sm.gx[g] = 0.0;
+          sm.gy[g] = 0.0;
+          ++g;
+        }
+        if ((pst_mask >> k) & 1u) {
+          sm.pfirst[p] = (uint16_t)(g - 1);
+          ++p;
+        }
+      }
+    }
+  }
+  if (t == 0) sm.gpos[gtot] = (uint16_t)m;
+  __syncthreads();
+
+  // Rows: sampling decision + run-length accumulation per group.
+  {
+    int g = (int)gex - 1, p = (int)pex - 1;
+    int run_g = -1;
+    uint32_t run_c = 0;
+    double run_x = 0.0, run_y = 0.0;
+#pragma unroll
+    for (int k = 0; k < kSegItems; ++k) {
+      const int q = q0 + k;
+      if (q < m) {
+        if ((gst_mask >> k) & 1u) ++g;
+        if ((pst_mask >> k) & 1u) ++p;
+        const int gs = sm.gpos[g];
+        const int ng = (int)sm.gpos[g + 1] - gs;
+        const int j = q - gs;
+        const int grank = g - (int)sm.pfirst[p];
+        const int idx = (int)(keys[k] & ((1u << kIdxBits) - 1u));
+        const uint32_t pkr = sm.pk[idx];
+        const uint32_t pid = pid_base + (uint32_t)(keys[k] >> shift_p);
+        if (j == 0) {
+          sm.gpk[g] = pkr;
+          sm.gkeep[g] = (uint8_t)(grank < sp.l0);
+        }
+        bool kept = grank < sp.l0;
+        if (kept && ng > sp.linf)
+          kept = pdp::cycle_walk((uint32_t)j, (uint64_t)ng, pdp::group_perm_key(sp.seed, pid, pkr)) <
+                 (uint64_t)sp.linf;
+        if (kept) {
+          if (g != run_g) {
+            if (run_g >= 0) {
+              atomicAdd(&sm.gcnt[run_g], run_c);
+              if (sp.xmode != kXNone) atomicAdd(&sm.gx[run_g], run_x);
+              if (sp.want_y) atomicAdd(&sm.gy[run_g], run_y);
+            }
+            run_g = g;
+            run_c = 0;
+            run_x = 0.0;
+            run_y = 0.0;
+          }
+          double x, y;
+          row_terms(sp, sm.val[idx], x, y);
+          ++run_c;
+          run_x += x;
+          run_y += y;
+        }
+      }
+    }
+    if (run_g >= 0) {
+      atomicAdd(&sm.gcnt[run_g], run_c);
+      if (sp.xmode != kXNone) atomicAdd(&sm.gx[run_g], run_x);
+      if (sp.want_y) atomicAdd(&sm.gy[run_g], run_y);
+    }
+  }
+  __syncthreads();
+
+  for (int g = t; g < (int)gtot; g += kThreads) {
+    if (sm.gkeep[g] && sm.gcnt[g] > 0) emit_group(sp, acc, sm.gpk[g], sm.gcnt[g], sm.gx[g], sm.gy[g]);
+  }
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(kThreads) void k_buckets(const Rec* __restrict__ recs,
+                                                      const unsigned long long* __restrict__ counters_n,
+                                                      int n_slot, SegParams sp, AccPtrs acc, OvList ov,
+                                                      int force_fallback) {
+  __shared__ BucketSmem sm;
+  const int t = threadIdx.x;
+  const int64_t n = (int64_t)counters_n[n_slot];
+  const int64_t lo = (int64_t)blockIdx.x * kSegCap;
+  if (lo >= n) return;
+  const int64_t hi = lo + kSegCap < n ? lo + kSegCap : n;
+  const int64_t kNone = INT64_MAX;
+
+  int64_t s = kNone;
+  for (int64_t p = lo + t; p < hi; p += kThreads)
+    if (is_bucket_start(recs, p, n, sp.low)) {
+      s = p;
+      break;
+    }
+  s = block_min(s, sm.tmp64);
+  if (s == kNone) return;
+
+  int64_t cur = s;
+  while (cur < hi) {
+    const int64_t wend = cur + kSegCap < n ? cur + kSegCap : n;
+    int64_t fgh = kNone;
+    for (int64_t p = cur + 1 + t; p <= wend; p += kThreads)
+      if (p >= hi && is_bucket_start(recs, p, n, sp.low)) {
+        fgh = p;
+        break;
+      }
+    fgh = block_min(fgh, sm.tmp64);
+    const int64_t limit = fgh < wend ? fgh : wend;
+    int64_t be = -1;
+    for (int64_t p = cur + 1 + t; p <= limit; p += kThreads)
+      if (is_bucket_start(recs, p, n, sp.low)) be = p;
+    be = block_max(be, sm.tmp64);
+    if (be < 0) {
+      // Bucket at cur is larger than one LDS batch: find its end.
+      int64_t bend = kNone;
+      for (int64_t chunk = wend + 1; bend == kNone; chunk += kThreads) {
+        int64_t c = kNone;
+        const int64_t p = chunk + t;
+        if (p <= n && is_bucket_start(recs, p, n, sp.low)) c = p;
+        bend = block_min(c, sm.tmp64);
+      }
+      if (t == 0) record_overflow(ov, cur, bend);
+      cur = bend;
+      continue;
+    }
+    if (force_fallback) {
+      if (t == 0) record_overflow(ov, cur, be);
+    } else {
+      process_batch(recs, cur, be, sp, acc, ov, sm);
+    }
+    cur = be;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// KF: generic sorted-stream path (fallback for buckets that overflow LDS)
+// ---------------------------------------------------------------------------
+
+__global__ void k_gather_ranges(const Rec* __restrict__ src, Rec* __restrict__ dst,
+                                const long long* __restrict__ rsrc, const long long* __restrict__ rdst,
+                                int nranges, int64_t total) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    int lo = 0, hi = nranges - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (rdst[mid] <= i) lo = mid; else hi = mid - 1;
+    }
+    dst[i] = src[rsrc[lo] + (i - rdst[lo])];
+  }
+}
+
+__global__ void k_stream_flags(const Rec* __restrict__ r, int64_t m, long long* __restrict__ gs,
+                               long long* __restrict__ ps) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (int64_t)gridDim.x * blockDim.x) {
+    const Rec a = r[i];
+    bool g = true, p = true;
+    if (i > 0) {
+      const Rec b = r[i - 1];
+      p = a.pid != b.pid;
+      g = p || a.pk != b.pk;
+    }
+    gs[i] = g;
+    ps[i] = p;
+  }
+}
+
+// Inclusive scan of 2048-element chunks; chunk totals to sums.
+__global__ __launch_bounds__(kThreads) void k_scan_chunks(long long* __restrict__ a, int64_t n,
+                                                          long long* __restrict__ sums) {
+  __shared__ long long s_tmp[4];
+  const int64_t base = (int64_t)blockIdx.x * 2048 + threadIdx.x * 8;
+  long long v[8];
+  long long acc = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    v[k] = base + k < n ? a[base + k] : 0;
+    acc += v[k];
+    v[k] = acc;
+  }
+  long long tot;
+  const long long ex = block_excl_scan(acc, s_tmp, tot);
+#pragma unroll
+  for (int k = 0; k < 8; ++k)
+    if (base + k < n) a[base + k] = v[k] + ex;
+  if (threadIdx.x == 0) sums[blockIdx.x] = tot;
+}
+
+__global__ void k_scan_add(long long* __restrict__ a, int64_t n, const long long* __restrict__ sums) {
+  if (blockIdx.x == 0) return;
+  const long long add = sums[blockIdx.x - 1];
+  const int64_t base = (int64_t)blockIdx.x * 2048;
+  for (int k = threadIdx.x; k < 2048; k += blockDim.x)
+    if (base + k < n) a[base + k] += add;
+}
+
+__global__ void k_stream_starts(const long long* __restrict__ gs_raw_scan, const long long* __restrict__ ps_scan,
+                                const Rec* __restrict__ r, int64_t m, long long* __restrict__ gpos,
+                                long long* __restrict__ pfirst) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (int64_t)gridDim.x * blockDim.x) {
+    const long long g = gs_raw_scan[i] - 1;
+    const long long p = ps_scan[i] - 1;
+    const bool gstart = i == 0 || gs_raw_scan[i - 1] != gs_raw_scan[i];
+    const bool pstart = i == 0 || ps_scan[i - 1] != ps_scan[i];
+    if (gstart) gpos[g] = i;
+    if (pstart) pfirst[p] = g;
+    if (i == m - 1) gpos[g + 1] = m;
+  }
+}
+
+__global__ void k_stream_rows(const Rec* __restrict__ r, int64_t m, const long long* __restrict__ gsc,
+                              const long long* __restrict__ psc, const long long* __restrict__ gpos,
+                              const long long* __restrict__ pfirst, SegParams sp,
+                              unsigned long long* __restrict__ gcnt, double* __restrict__ gx,
+                              double* __restrict__ gy) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (int64_t)gridDim.x * blockDim.x) {
+    const long long g = gsc[i] - 1, p = psc[i] - 1;
+    const long long grank = g - pfirst[p];
+    if (grank >= sp.l0) continue;
+    const long long gs0 = gpos[g];
+    const long long ng = gpos[g + 1] - gs0;
+    const long long j = i - gs0;
+    const Rec a = r[i];
+    bool kept = true;
+    if (ng > sp.linf)
+      kept = pdp::cycle_walk((uint32_t)j, (uint64_t)ng, pdp::group_perm_key(sp.seed, a.pid, a.pk)) <
+             (uint64_t)sp.linf;
+    if (!kept) continue;
+    double x, y;
+    row_terms(sp, a.val, x, y);
+    atomicAdd(&gcnt[g], 1ull);
+    if (sp.xmode != kXNone) atomicAdd(&gx[g], x);
+    if (sp.want_y) atomicAdd(&gy[g], y);
+  }
+}
+
+__global__ void k_stream_groups(const Rec* __restrict__ r, const long long* __restrict__ psc,
+                                const long long* __restrict__ gpos, const long long* __restrict__ pfirst,
+                                int64_t ngroups, SegParams sp, const unsigned long long* __restrict__ gcnt,
+                                const double* __restrict__ gx, const double* __restrict__ gy, AccPtrs acc) {
+  for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < ngroups;
+       g += (int64_t)gridDim.x * blockDim.x) {
+    const long long q = gpos[g];
+    const long long p = psc[q] - 1;
+    if (g - pfirst[p] >= sp.l0 || gcnt[g] == 0) continue;
+    emit_group(sp, acc, r[q].pk, (uint32_t)gcnt[g], gx[g], gy[g]);
+  }
+}
+
+// contribution_bounds_already_enforced: every row is its own accumulator
+// (dp_engine.py:139-150, combiners.py create_accumulator([value])).
+__global__ void k_enforced(const int64_t* __restrict__ pk, const double* __restrict__ val, int64_t n,
+                           int64_t num_parts, SegParams sp, AccPtrs acc, unsigned long long* __restrict__ counters) {
+  unsigned int invalid = 0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t b = pk[i];
+    if (b < 0) continue;
+    if (b >= num_parts) {
+      ++invalid;
+      continue;
+    }
+    double x = 0.0, y = 0.0;
+    if (sp.has_value) {
+      row_terms(sp, val[i], x, y);
+    }
+    emit_group(sp, acc, (uint32_t)b, 1u, x, y);
+  }
+  if (invalid) atomicAdd(&counters[kCtrInvalid], (unsigned long long)invalid);
+}
+
+// ---------------------------------------------------------------------------
+// K5/K6: partition selection + noisy metrics, one thread per partition
+// ---------------------------------------------------------------------------
+
+struct RelParams {
+  int metrics, kind, selection, add_noise;
+  int nfields;
+  int field[5];
+  double s_count, s_sum, s_mean_count, s_mean_nsum, s_var_nsq, s_pid;
+  int sum_zero, mean_degenerate, sq_degenerate;
+  double a, mid, sq_a, sq_mid;
+  double sel_thr, sel_scale;
+  const double* table;
+  int64_t tlen;
+  int64_t max_rows;
+  uint64_t seed;
+};
+
+__device__ __forceinline__ double noise(const RelParams& rp, uint64_t idx, uint32_t stream, double scale) {
+  if (!rp.add_noise || scale == 0.0) return 0.0;
+  return scale * (rp.kind == PDP_NOISE_LAPLACE ? pdp::unit_laplace(rp.seed, idx, stream)
+                                               : pdp::unit_gaussian(rp.seed, idx, stream));
+}
+
+__global__ void k_release(const unsigned long long* __restrict__ row_count,
+                          const unsigned long long* __restrict__ count, const double* __restrict__ xs,
+                          const double* __restrict__ ys, int64_t P, int64_t pk_offset, RelParams rp,
+                          uint8_t* __restrict__ keep, double* __restrict__ out) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < P; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t gidx = (uint64_t)(pk_offset + i);
+    const long long rc = (long long)row_count[i];
+    uint8_t kp = 1;
+    if (rp.selection != PDP_SELECTION_NONE) {
+      const long long nn = (rc + rp.max_rows - 1) / rp.max_rows;
+      if (nn <= 0) {
+        kp = 0;
+      } else if (rp.selection == PDP_SELECTION_TRUNCATED_GEOMETRIC) {
+        const double p = nn < rp.tlen ? rp.table[nn] : 1.0;
+        if (rp.add_noise) {
+          double u, u2;
+          pdp::philox_uniforms(rp.seed, gidx, pdp::kStreamSelect, u, u2);
+          kp = u < p;
+        } else {
+          kp = p > 0.0;
+        }
+      } else {
+        double z = 0.0;
+        if (rp.add_noise)
+          z = rp.selection == PDP_SELECTION_LAPLACE_THRESHOLDING
+                  ? pdp::unit_laplace(rp.seed, gidx, pdp::kStreamSelect)
+                  : pdp::unit_gaussian(rp.seed, gidx, pdp::kStreamSelect);
+        kp = ((double)nn + rp.sel_scale * z) > rp.sel_thr;
+      }
+    }
+    keep[i] = kp;
+    double f[5] = {0, 0, 0, 0, 0};  // variance, mean, count, sum, pid_count
+    const int m = rp.metrics;
+    if (m & (PDP_METRIC_VARIANCE | PDP_METRIC_MEAN)) {
+      const double dp_count = (double)(long long)count[i] + noise(rp, gidx, pdp::kStreamMeanCount, rp.s_mean_count);
+      const double denom = dp_count > 1.0 ? dp_count : 1.0;
+      double dp_mean;
+      if (rp.mean_degenerate) {
+        dp_mean = rp.a;
+      } else {
+        dp_mean = (xs[i] + noise(rp, gidx, pdp::kStreamMeanNsum, rp.s_mean_nsum)) / denom;
+      }
+      if (m & PDP_METRIC_VARIANCE) {
+        double msq;
+        if (rp.sq_degenerate)
+          msq = rp.sq_a;
+        else
+          msq = (ys[i] + noise(rp, gidx, pdp::kStreamVarNsq, rp.s_var_nsq)) / denom;
+        f[0] = msq - dp_mean * dp_mean;
+      }
+      if (!rp.mean_degenerate) dp_mean += rp.mid;
+      f[1] = dp_mean;
+      f[2] = dp_count;
+      f[3] = dp_mean * dp_count;
+    } else {
+      if (m & PDP_METRIC_COUNT)
+        f[2] = (double)(long long)count[i] + noise(rp, gidx, pdp::kStreamCount, rp.s_count);
+      if (m & PDP_METRIC_SUM) f[3] = rp.sum_zero ? 0.0 : xs[i] + noise(rp, gidx, pdp::kStreamSum, rp.s_sum);
+    }
+    if (m & PDP_METRIC_PRIVACY_ID_COUNT) f[4] = (double)rc + noise(rp, gidx, pdp::kStreamPidCount, rp.s_pid);
+    for (int k = 0; k < rp.nfields; ++k) out[(int64_t)k * P + i] = f[rp.field[k]];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Synthetic generator (oracle/pdp_oracle.py:synth_rows)
+// ---------------------------------------------------------------------------
+
+__global__ void k_generate(int64_t* __restrict__ pid, int64_t* __restrict__ pk, double* __restrict__ value, int64_t n,
+                           int64_t row_offset, int64_t U, int64_t P, double zipf_s, int value_kind, double lo,
+                           double hi, uint64_t seed) {
+  const int pkb = P > 1 ? pdp::ceil_log2_u64((uint64_t)P) : 1;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t gi = (uint64_t)(row_offset + i);
+    pdp::u32x4 c{(uint32_t)gi, (uint32_t)(gi >> 32), pdp::kStreamSynth, 0u};
+    const pdp::u32x4 x = pdp::philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+    const double inv = 1.0 / 4294967296.0;
+    const double u0 = ((double)x.x + 0.5) * inv, u1 = ((double)x.y + 0.5) * inv, u2 = ((double)x.z + 0.5) * inv;
+    int64_t a = (int64_t)(u0 * (double)U);
+    if (a > U - 1) a = U - 1;
+    int64_t b;
+    if (zipf_s > 0.0) {
+      const double tt = 1.0 - zipf_s;
+      const double top = pow((double)P + 1.0, tt);
+      const double xr = pow(1.0 + u1 * (top - 1.0), 1.0 / tt);
+      int64_t rank = (int64_t)floor(xr) - 1;
+      rank = rank < 0 ? 0 : (rank > P - 1 ? P - 1 : rank);
+      uint32_t y = pdp::perm_bits((uint32_t)rank, pkb, 0x5A495046ull);
+      while ((int64_t)y >= P) y = pdp::perm_bits(y, pkb, 0x5A495046ull);
+      b = y;
+    } else {
+      b = (int64_t)(u1 * (double)P);
+      if (b > P - 1) b = P - 1;
+    }
+    pid[i] = a;
+    pk[i] = b;
+    if (value) {
+      if (value_kind == 1) {
+        int64_t rr = (int64_t)(u2 * 5.0);
+        rr = rr > 4 ? 4 : rr;
+        value[i] = 1.0 + (double)rr;
+      } else {
+        value[i] = lo + u2 * (hi - lo);
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Host side
+// ---------------------------------------------------------------------------
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                              \
+  do {                                                                                             \
+    hipError_t e_ = (expr);                                                                        \
+    if (e_ != hipSuccess) return fail(PDP_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+int grid_for(int64_t n, int threads, int cap = 4096) {
+  int64_t g = (n + threads - 1) / threads;
+  if (g < 1) g = 1;
+  if (g > cap) g = cap;
+  return (int)g;
+}
+
+struct Layout {
+  size_t recs_a, recs_b, hist, off, counters, status, ranges, total;
+  int64_t tiles;
+};
+
+Layout layout_for(int64_t n) {
+  Layout L{};
+  size_t o = 0;
+  const size_t rb = align_up((size_t)std::max<int64_t>(n, 1) * sizeof(Rec), 256);
+  L.recs_a = o; o += rb;
+  L.recs_b = o; o += rb;
+  L.hist = o; o += align_up(kMaxPasses * kHist * 8, 256);
+  L.off = o; o += align_up(kMaxPasses * kHist * 8, 256);
+  L.counters = o; o += align_up(kNumCounters * 8, 256);
+  L.tiles = (std::max<int64_t>(n, 1) + kTile - 1) / kTile;
+  L.status = o; o += align_up((size_t)L.tiles * kStatusStride * 8, 256);
+  L.ranges = o; o += align_up((size_t)kOverflowCap * 16, 256);
+  L.total = o;
+  return L;
+}
+
+struct Plan {
+  int pidb, pkb, low, passes;
+  int bits[kMaxPasses];
+};
+
+Plan make_plan(int64_t n, int64_t U, int64_t P) {
+  Plan p{};
+  p.pidb = std::max(1, pdp::ceil_log2_u64((uint64_t)U));
+  p.pkb = std::max(1, pdp::ceil_log2_u64((uint64_t)P));
+  const double rows_per_pid = (double)n / (double)U;
+  p.low = 0;
+  while (p.low < p.pidb && rows_per_pid * (double)(1ull << (p.low + 1)) <= kBucketTarget) ++p.low;
+  const int kb = p.pidb - p.low;
+  p.passes = std::max(1, (kb + 7) / 8);
+  int rem = kb;
+  for (int i = 0; i < p.passes; ++i) {
+    const int w = (rem + (p.passes - i) - 1) / (p.passes - i);
+    p.bits[i] = w;
+    rem -= w;
+  }
+  return p;
+}
+
+SegParams make_seg(const pdp_bound_params* bp, int low, int pkb, bool has_value) {
+  SegParams sp{};
+  sp.low = low;
+  sp.pkb = pkb;
+  sp.seed = bp->sampling_seed;
+  sp.l0 = bp->max_partitions_contributed;
+  sp.linf = bp->max_contributions_per_partition;
+  const int m = bp->metrics;
+  sp.want_count = (m & (PDP_METRIC_COUNT | PDP_METRIC_MEAN | PDP_METRIC_VARIANCE)) != 0;
+  sp.has_value = has_value;
+  sp.xmode = kXNone;
+  sp.want_y = 0;
+  if (m & (PDP_METRIC_MEAN | PDP_METRIC_VARIANCE)) {
+    sp.xmode = kXNsum;
+    sp.want_y = (m & PDP_METRIC_VARIANCE) != 0;
+  } else if (m & PDP_METRIC_SUM) {
+    sp.xmode = bp->has_value_bounds ? kXClipSum : kXRawSum;
+  }
+  sp.a = bp->min_value;
+  sp.b = bp->max_value;
+  sp.mid = bp->min_value + (bp->max_value - bp->min_value) / 2;  // dp_computations.py:65-69
+  sp.smin = bp->min_sum_per_partition;
+  sp.smax = bp->max_sum_per_partition;
+  return sp;
+}
+
+}  // namespace
+
+struct pdp_ctx {
+  int device = 0;
+  bool prof = false;
+  struct ProfRec {
+    int stage;
+    hipEvent_t a, b;
+  };
+  std::vector<ProfRec> pending;
+  std::vector<hipEvent_t> pool;
+  double prof_ms[PDP_NUM_STAGES] = {};
+  int64_t prof_n[PDP_NUM_STAGES] = {};
+  void* last_ws = nullptr;
+  uint32_t epoch = 0;
+  pdp_stats stats{};
+  std::vector<double> table_host;
+  double* table_dev = nullptr;
+  size_t table_cap = 0;
+  double table_key[3] = {-1, -1, -1};
+  int64_t table_len = 0;
+};
+
+namespace {
+
+hipEvent_t prof_event(pdp_ctx* ctx) {
+  if (!ctx->pool.empty()) {
+    hipEvent_t e = ctx->pool.back();
+    ctx->pool.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  (void)hipEventCreate(&e);
+  return e;
+}
+
+// Records hipEvents around a stage on `stream` when profiling is enabled.
+struct ProfScope {
+  pdp_ctx* ctx;
+  int stage;
+  hipStream_t stream;
+  hipEvent_t a = nullptr;
+  ProfScope(pdp_ctx* c, int s, hipStream_t st) : ctx(c), stage(s), stream(st) {
+    if (ctx->prof) {
+      a = prof_event(ctx);
+      (void)hipEventRecord(a, stream);
+    }
+  }
+  ~ProfScope() {
+    if (ctx->prof && a) {
+      hipEvent_t b = prof_event(ctx);
+      (void)hipEventRecord(b, stream);
+      ctx->pending.push_back({stage, a, b});
+    }
+  }
+};
+
+int next_epoch(pdp_ctx* ctx, hipStream_t stream, unsigned long long* status, size_t status_bytes, void* ws) {
+  if (ctx->last_ws != ws || ctx->epoch >= 0xFFFE) {
+    HIP_TRY(hipMemsetAsync(status, 0, status_bytes, stream));
+    ctx->last_ws = ws;
+    ctx->epoch = 0;
+  }
+  ++ctx->epoch;
+  return 0;
+}
+
+int scan_inplace(long long* a, int64_t n, hipStream_t stream) {
+  if (n <= 0) return 0;
+  const int64_t nb = (n + 2047) / 2048;
+  long long* sums = nullptr;
+  HIP_TRY(hipMallocAsync((void**)&sums, (size_t)nb * sizeof(long long), stream));
+  hipLaunchKernelGGL(k_scan_chunks, dim3((unsigned)nb), dim3(kThreads), 0, stream, a, n, sums);
+  if (nb > 1) {
+    int rc = scan_inplace(sums, nb, stream);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_scan_add, dim3((unsigned)nb), dim3(kThreads), 0, stream, a, n, sums);
+  }
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipFreeAsync(sums, stream));
+  return 0;
+}
+
+// Full LSD sort of `m` records in `a` by (pid, pi_pid(pk)); result pointer
+// returned via out (either a or b).
+int sort_pid_pk(pdp_ctx* ctx, Rec* a, Rec* b, int64_t m, const Plan& plan, uint64_t seed, uint32_t U, uint32_t P,
+                unsigned long long* hist, unsigned long long* off, unsigned long long* counters,
+                unsigned long long* status, size_t status_bytes, void* ws, int tile_slot0, hipStream_t stream,
+                Rec** out) {
+  KeySpec ks{};
+  ks.mode = 1;
+  ks.low = 0;
+  ks.pkb = plan.pkb;
+  ks.seed = seed;
+  ks.num_pids = U;
+  ks.num_parts = P;
+  const int kb = plan.pidb + plan.pkb;
+  ks.passes = (kb + 7) / 8;
+  int sh = 0;
+  for (int i = 0; i < ks.passes; ++i) {
+    ks.shift[i] = sh;
+    ks.bits[i] = std::min(8, kb - sh);
+    sh += ks.bits[i];
+  }
+  HIP_TRY(hipMemsetAsync(hist, 0, kMaxPasses * kHist * 8, stream));
+  ProfScope prof_generic(ctx, PDP_STAGE_GENERIC, stream);
+  hipLaunchKernelGGL(k_histogram<false>, dim3(grid_for(m, kThreads, 2048)), dim3(kThreads), 0, stream,
+                     (const int64_t*)nullptr, (const int64_t*)nullptr, a, m, ks, hist, counters);
+  hipLaunchKernelGGL(k_offsets, dim3(1), dim3(kThreads), 0, stream, hist, off, ks.passes, m, counters,
+                     (int)kCtrNGeneric);
+  Rec* src = a;
+  Rec* dst = b;
+  const int64_t tiles = (m + kTile - 1) / kTile;
+  for (int p = 0; p < ks.passes; ++p) {
+    int rc = next_epoch(ctx, stream, status, status_bytes, ws);
+    if (rc) return rc;
+    if (tile_slot0 + p >= (int)kNumCounters) return fail(PDP_ERR_INTERNAL, "too many radix passes");
+    hipLaunchKernelGGL(k_onesweep<false>, dim3((unsigned)tiles), dim3(kThreads), 0, stream,
+                       (const int64_t*)nullptr, (const int64_t*)nullptr, (const double*)nullptr, src, dst, m,
+                       counters, (int)kCtrNGeneric, ks, p, off + p * kHist, status, ctx->epoch, counters,
+                       tile_slot0 + p);
+    std::swap(src, dst);
+  }
+  HIP_TRY(hipGetLastError());
+  *out = src;
+  return 0;
+}
+
+int run_generic(pdp_ctx* ctx, Rec* sorted, Rec* spare, const std::vector<unsigned long long>& ranges,
+                const Plan& plan, const SegParams& sp, const pdp_bound_params* bp, uint32_t U, uint32_t P,
+                AccPtrs acc, unsigned long long* hist, unsigned long long* off, unsigned long long* counters,
+                unsigned long long* status, size_t status_bytes, void* ws, hipStream_t stream) {
+  const int nr = (int)(ranges.size() / 2);
+  std::vector<long long> rsrc(nr), rdst(nr);
+  int64_t total = 0;
+  for (int i = 0; i < nr; ++i) {
+    rsrc[i] = (long long)ranges[2 * i];
+    rdst[i] = total;
+    total += (int64_t)(ranges[2 * i + 1] - ranges[2 * i]);
+  }
+  ctx->stats.fallback_rows = total;
+  ctx->stats.fallback_ranges = nr;
+  if (total == 0) return 0;
+  long long *d_rsrc = nullptr, *d_rdst = nullptr;
+  HIP_TRY(hipMallocAsync((void**)&d_rsrc, nr * sizeof(long long), stream));
+  HIP_TRY(hipMallocAsync((void**)&d_rdst, nr * sizeof(long long), stream));
+  HIP_TRY(hipMemcpyAsync(d_rsrc, rsrc.data(), nr * sizeof(long long), hipMemcpyHostToDevice, stream));
+  HIP_TRY(hipMemcpyAsync(d_rdst, rdst.data(), nr * sizeof(long long), hipMemcpyHostToDevice, stream));
+  hipLaunchKernelGGL(k_gather_ranges, dim3(grid_for(total, kThreads)), dim3(kThreads), 0, stream, sorted, spare,
+                     d_rsrc, d_rdst, nr, total);
+  HIP_TRY(hipStreamSynchronize(stream));  // host vectors go out of scope
+  HIP_TRY(hipFreeAsync(d_rsrc, stream));
+  HIP_TRY(hipFreeAsync(d_rdst, stream));
+
+  Rec* r = nullptr;
+  int rc = sort_pid_pk(ctx, spare, sorted, total, plan, bp->sampling_seed, U, P, hist, off, counters, status,
+                       status_bytes, ws, kCtrTile0 + 16, stream, &r);
+  if (rc) return rc;
+
+  long long *gsc, *psc, *gpos, *pfirst;
+  unsigned long long* gcnt;
+  double *gx, *gy;
+  const size_t m8 = (size_t)total * 8;
+  HIP_TRY(hipMallocAsync((void**)&gsc, m8, stream));
+  HIP_TRY(hipMallocAsync((void**)&psc, m8, stream));
+  HIP_TRY(hipMallocAsync((void**)&gpos, m8 + 8, stream));
+  HIP_TRY(hipMallocAsync((void**)&pfirst, m8, stream));
+  HIP_TRY(hipMallocAsync((void**)&gcnt, m8, stream));
+  HIP_TRY(hipMallocAsync((void**)&gx, m8, stream));
+  HIP_TRY(hipMallocAsync((void**)&gy, m8, stream));
+  HIP_TRY(hipMemsetAsync(gcnt, 0, m8, stream));
+  HIP_TRY(hipMemsetAsync(gx, 0, m8, stream));
+  HIP_TRY(hipMemsetAsync(gy, 0, m8, stream));
+  const int gr = grid_for(total, kThreads);
+  hipLaunchKernelGGL(k_stream_flags, dim3(gr), dim3(kThreads), 0, stream, r, total, gsc, psc);
+  rc = scan_inplace(gsc, total, stream);
+  if (rc) return rc;
+  rc = scan_inplace(psc, total, stream);
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_stream_starts, dim3(gr), dim3(kThreads), 0, stream, gsc, psc, r, total, gpos, pfirst);
+  long long ngroups = 0;
+  HIP_TRY(hipMemcpyAsync(&ngroups, gsc + (total - 1), 8, hipMemcpyDeviceToHost, stream));
+  hipLaunchKernelGGL(k_stream_rows, dim3(gr), dim3(kThreads), 0, stream, r, total, gsc, psc, gpos, pfirst, sp, gcnt,
+                     gx, gy);
+  HIP_TRY(hipStreamSynchronize(stream));
+  hipLaunchKernelGGL(k_stream_groups, dim3(grid_for(ngroups, kThreads)), dim3(kThreads), 0, stream, r, psc, gpos,
+                     pfirst, (int64_t)ngroups, sp, gcnt, gx, gy, acc);
+  HIP_TRY(hipGetLastError());
+  for (void* p : {(void*)gsc, (void*)psc, (void*)gpos, (void*)pfirst, (void*)gcnt, (void*)gx, (void*)gy})
+    HIP_TRY(hipFreeAsync(p, stream));
+  return 0;
+}
+
+double std_normal_cdf(double x) { return 0.5 * std::erfc(-x / std::sqrt(2.0)); }
+
+double gaussian_delta(double sigma, double eps) {
+  const double a = 1.0 / (2.0 * sigma), b = eps * sigma;
+  return std_normal_cdf(a - b) - std::exp(eps) * std_normal_cdf(-a - b);
+}
+
+// Acklam's inverse normal CDF refined by one Halley step.
+double norm_ppf(double p) {
+  static const double a[] = {-3.969683028665376e+01, 2.209460984245205e+02, -2.759285104469687e+02,
+                             1.383577518672690e+02, -3.066479806614716e+01, 2.506628277459239e+00};
+  static const double b[] = {-5.447609879822406e+01, 1.615858368580409e+02, -1.556989798598866e+02,
+                             6.680131188771972e+01, -1.328068155288572e+01};
+  static const double c[] = {-7.784894002430293e-03, -3.223964580411365e-01, -2.400758277161838e+00,
+                             -2.549732539343734e+00, 4.374664141464968e+00, 2.938163982698783e+00};
+  static const double d[] = {7.784695709041462e-03, 3.224671290700398e-01, 2.445134137142996e+00,
+                             3.754408661907416e+00};
+  double x;
+  if (p < 0.02425) {
+    const double q = std::sqrt(-2 * std::log(p));
+    x = (((((c[0] * q + c[1]) * q + c[2]) * q + c[3]) * q + c[4]) * q + c[5]) /
+        ((((d[0] * q + d[1]) * q + d[2]) * q + d[3]) * q + 1);
+  } else if (p > 1 - 0.02425) {
+    const double q = std::sqrt(-2 * std::log(1 - p));
+    x = -(((((c[0] * q + c[1]) * q + c[2]) * q + c[3]) * q + c[4]) * q + c[5]) /
+        ((((d[0] * q + d[1]) * q + d[2]) * q + d[3]) * q + 1);
+  } else {
+    const double q = p - 0.5, r = q * q;
+    x = (((((a[0] * r + a[1]) * r + a[2]) * r + a[3]) * r + a[4]) * r + a[5]) * q /
+        (((((b[0] * r + b[1]) * r + b[2]) * r + b[3]) * r + b[4]) * r + 1);
+  }
+  const double e = std_normal_cdf(x) - p;
+  const double u = e * std::sqrt(2 * M_PI) * std::exp(x * x / 2);
+  return x - u / (1 + x * u / 2);
+}
+
+double noise_scale(int kind, double eps, double delta, double l0, double linf) {
+  // dp_computations.py:146-175
+  if (kind == PDP_NOISE_LAPLACE) return l0 * linf / eps;
+  return pdp_gaussian_sigma(eps, delta, std::sqrt(l0) * linf);
+}
+
+}  // namespace
+
+extern "C" {
+
+int pdp_abi_version(void) { return PDP_ABI_VERSION; }
+
+const char* pdp_last_error(void) { return g_err.c_str(); }
+
+pdp_ctx* pdp_ctx_create(int device) {
+  pdp_ctx* c = new pdp_ctx();
+  c->device = device;
+  return c;
+}
+
+void pdp_ctx_destroy(pdp_ctx* ctx) {
+  if (!ctx) return;
+  for (auto& r : ctx->pending) {
+    (void)hipEventDestroy(r.a);
+    (void)hipEventDestroy(r.b);
+  }
+  for (auto e : ctx->pool) (void)hipEventDestroy(e);
+  if (ctx->table_dev) (void)hipFree(ctx->table_dev);
+  delete ctx;
+}
+
+int pdp_metric_fields(int32_t metrics, int32_t* fields) {
+  int n = 0;
+  if (metrics & PDP_METRIC_VARIANCE) {
+    fields[n++] = PDP_FIELD_VARIANCE;  // VarianceCombiner dict order, combiners.py:386-392
+    if (metrics & PDP_METRIC_COUNT) fields[n++] = PDP_FIELD_COUNT;
+    if (metrics & PDP_METRIC_SUM) fields[n++] = PDP_FIELD_SUM;
+    if (metrics & PDP_METRIC_MEAN) fields[n++] = PDP_FIELD_MEAN;
+  } else if (metrics & PDP_METRIC_MEAN) {
+    fields[n++] = PDP_FIELD_MEAN;  // combiners.py:323-328
+    if (metrics & PDP_METRIC_COUNT) fields[n++] = PDP_FIELD_COUNT;
+    if (metrics & PDP_METRIC_SUM) fields[n++] = PDP_FIELD_SUM;
+  } else {
+    if (metrics & PDP_METRIC_COUNT) fields[n++] = PDP_FIELD_COUNT;
+    if (metrics & PDP_METRIC_SUM) fields[n++] = PDP_FIELD_SUM;
+  }
+  if (metrics & PDP_METRIC_PRIVACY_ID_COUNT) fields[n++] = PDP_FIELD_PRIVACY_ID_COUNT;
+  return n;
+}
+
+double pdp_gaussian_sigma(double eps, double delta, double l2) {
+  // PyDP GaussianMechanism std (see oracle/pdp_oracle.py:gaussian_sigma).
+  if (!(eps > 0) || !(delta > 0)) return NAN;
+  double lo = 0.0, hi = 1.0;
+  while (gaussian_delta(hi, eps) > delta) {
+    lo = hi;
+    hi *= 2.0;
+  }
+  while (hi - lo > 1e-3 * lo) {
+    const double mid = lo + (hi - lo) / 2.0;
+    if (gaussian_delta(mid, eps) > delta)
+      lo = mid;
+    else
+      hi = mid;
+  }
+  return hi * l2;
+}
+
+int pdp_truncated_geometric_table(double eps, double delta, int64_t k, double* out, int64_t cap, int64_t* length) {
+  if (!(eps > 0) || delta < 0 || k <= 0 || !length) return fail(PDP_ERR_INVALID_ARG, "bad truncated geometric args");
+  const double e = eps / (double)k, d = delta / (double)k;
+  const double ee = std::exp(e), eme = std::exp(-e);
+  double prev = 0.0;
+  int64_t len = 1;
+  if (out && cap > 0) out[0] = 0.0;
+  while (prev < 1.0) {
+    double nxt = std::min(std::min(ee * prev + d, 1.0 - eme * (1.0 - prev - d)), 1.0);
+    if (nxt <= prev) return fail(PDP_ERR_INVALID_ARG, "truncated geometric selection cannot keep partitions");
+    if (out && len < cap) out[len] = nxt;
+    ++len;
+    prev = nxt;
+    if (len > (1ll << 24)) return fail(PDP_ERR_INVALID_ARG, "truncated geometric table too long");
+  }
+  *length = len;
+  return 0;
+}
+
+int pdp_selection_threshold(int32_t selection, double eps, double delta, int64_t k, double* thr, double* scale) {
+  if (!(eps > 0) || k <= 0) return fail(PDP_ERR_INVALID_ARG, "bad selection args");
+  if (selection == PDP_SELECTION_LAPLACE_THRESHOLDING) {
+    const double adj = 1.0 - std::pow(1.0 - delta, 1.0 / (double)k);
+    const double b = (double)k / eps;
+    *scale = b;
+    *thr = adj > 0.5 ? 1.0 + b * std::log(2.0 * (1.0 - adj)) : 1.0 - b * std::log(2.0 * adj);
+    return 0;
+  }
+  if (selection == PDP_SELECTION_GAUSSIAN_THRESHOLDING) {
+    if (!(delta > 0)) return fail(PDP_ERR_INVALID_ARG, "Gaussian thresholding needs delta > 0");
+    const double td = delta / 2.0, nd = delta - td;
+    const double sigma = pdp_gaussian_sigma(eps, nd, std::sqrt((double)k));
+    const double adj = 1.0 - std::pow(1.0 - td, 1.0 / (double)k);
+    *scale = sigma;
+    *thr = 1.0 + sigma * norm_ppf(1.0 - adj);
+    return 0;
+  }
+  return fail(PDP_ERR_INVALID_ARG, "selection has no threshold");
+}
+
+int pdp_workspace_size(const pdp_columns* cols, const pdp_bound_params* bp, size_t* bytes) {
+  if (!cols || !bp || !bytes) return fail(PDP_ERR_INVALID_ARG, "null argument");
+  if (cols->num_rows < 0) return fail(PDP_ERR_INVALID_ARG, "num_rows < 0");
+  *bytes = layout_for(cols->num_rows).total;
+  return 0;
+}
+
+int pdp_get_stats(pdp_ctx* ctx, pdp_stats* out) {
+  if (!ctx || !out) return fail(PDP_ERR_INVALID_ARG, "null argument");
+  *out = ctx->stats;
+  return 0;
+}
+
+int pdp_bound_accumulate(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp,
+                         const pdp_accumulators* accp, void* workspace, size_t workspace_bytes, void* stream_) {
+  if (!ctx || !cols || !bp || !accp) return fail(PDP_ERR_INVALID_ARG, "null argument");
+  hipStream_t stream = (hipStream_t)stream_;
+  const int64_t n = cols->num_rows, U = cols->num_privacy_ids, P = cols->num_partitions;
+  if (n < 0 || P < 1 || P > (1ll << 31)) return fail(PDP_ERR_INVALID_ARG, "num_partitions must be in [1, 2^31]");
+  if (!bp->bounds_already_enforced && (U < 1 || U > (1ll << 32)))
+    return fail(PDP_ERR_INVALID_ARG, "num_privacy_ids must be in [1, 2^32]");
+  if (bp->max_partitions_contributed < 1 || bp->max_contributions_per_partition < 1)
+    return fail(PDP_ERR_INVALID_ARG, "contribution bounds must be positive");
+  const int m = bp->metrics;
+  const bool need_value = (m & (PDP_METRIC_SUM | PDP_METRIC_MEAN | PDP_METRIC_VARIANCE)) != 0;
+  if (need_value && !cols->value) return fail(PDP_ERR_INVALID_ARG, "value column required for SUM/MEAN/VARIANCE");
+  if (n > 0 && !cols->pk) return fail(PDP_ERR_INVALID_ARG, "pk column required");
+  if (!bp->bounds_already_enforced && n > 0 && !cols->pid) return fail(PDP_ERR_INVALID_ARG, "pid column required");
+  if (!accp->row_count) return fail(PDP_ERR_INVALID_ARG, "row_count accumulator required");
+  const Plan plan = make_plan(n, std::max<int64_t>(U, 1), P);
+  SegParams sp = make_seg(bp, plan.low, plan.pkb, cols->value != nullptr);
+  if (sp.want_count && !accp->count) return fail(PDP_ERR_INVALID_ARG, "count accumulator required");
+  if (sp.xmode != kXNone && !accp->x) return fail(PDP_ERR_INVALID_ARG, "x accumulator required");
+  if (sp.want_y && !accp->y) return fail(PDP_ERR_INVALID_ARG, "y accumulator required");
+  AccPtrs acc{(unsigned long long*)accp->row_count, (unsigned long long*)accp->count, accp->x, accp->y};
+  ctx->stats = pdp_stats{};
+  ctx->stats.bucket_low_bits = plan.low;
+
+  HIP_TRY(hipMemsetAsync(acc.row_count, 0, (size_t)P * 8, stream));
+  if (acc.count) HIP_TRY(hipMemsetAsync(acc.count, 0, (size_t)P * 8, stream));
+  if (acc.x) HIP_TRY(hipMemsetAsync(acc.x, 0, (size_t)P * 8, stream));
+  if (acc.y) HIP_TRY(hipMemsetAsync(acc.y, 0, (size_t)P * 8, stream));
+  if (n == 0) return 0;
+
+  const Layout L = layout_for(n);
+  if (!workspace || workspace_bytes < L.total) return fail(PDP_ERR_WORKSPACE, "workspace too small");
+  char* ws = (char*)workspace;
+  Rec* recs_a = (Rec*)(ws + L.recs_a);
+  Rec* recs_b = (Rec*)(ws + L.recs_b);
+  unsigned long long* hist = (unsigned long long*)(ws + L.hist);
+  unsigned long long* off = (unsigned long long*)(ws + L.off);
+  unsigned long long* counters = (unsigned long long*)(ws + L.counters);
+  unsigned long long* status = (unsigned long long*)(ws + L.status);
+  unsigned long long* ranges = (unsigned long long*)(ws + L.ranges);
+  const size_t status_bytes = (size_t)L.tiles * kStatusStride * 8;
+  HIP_TRY(hipMemsetAsync(ws + L.hist, 0, L.status - L.hist, stream));  // hist, off, counters
+
+  if (bp->bounds_already_enforced) {
+    {
+      ProfScope ps(ctx, PDP_STAGE_ENFORCED, stream);
+      hipLaunchKernelGGL(k_enforced, dim3(grid_for(n, kThreads, 8192)), dim3(kThreads), 0, stream, cols->pk,
+                       cols->value, n, P, sp, acc, counters);
+    }
+    HIP_TRY(hipGetLastError());
+    unsigned long long inv = 0;
+    HIP_TRY(hipMemcpyAsync(&inv, counters + kCtrInvalid, 8, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipStreamSynchronize(stream));
+    if (inv) return fail(PDP_ERR_OUT_OF_RANGE, "partition id >= num_partitions in input");
+    return 0;
+  }
+
+  KeySpec ks{};
+  ks.mode = 0;
+  ks.low = plan.low;
+  ks.pkb = plan.pkb;
+  ks.seed = bp->sampling_seed;
+  ks.num_pids = (uint32_t)std::min<int64_t>(U, 0xFFFFFFFFll);
+  ks.num_parts = (uint32_t)P;
+  ks.passes = plan.passes;
+  {
+    int sh = 0;
+    for (int i = 0; i < plan.passes; ++i) {
+      ks.shift[i] = sh;
+      ks.bits[i] = plan.bits[i];
+      sh += plan.bits[i];
+    }
+  }
+  ctx->stats.sort_passes = plan.passes;
+  {
+    ProfScope ps(ctx, PDP_STAGE_HISTOGRAM, stream);
+    hipLaunchKernelGGL(k_histogram<true>, dim3(grid_for(n, kThreads, 2048)), dim3(kThreads), 0, stream, cols->pid,
+                       cols->pk, (const Rec*)nullptr, n, ks, hist, counters);
+  }
+  hipLaunchKernelGGL(k_offsets, dim3(1), dim3(kThreads), 0, stream, hist, off, ks.passes, n, counters,
+                     (int)kCtrNKept);
+  Rec* src = nullptr;
+  Rec* dst = recs_a;
+  for (int p = 0; p < ks.passes; ++p) {
+    int rc = next_epoch(ctx, stream, status, status_bytes, workspace);
+    if (rc) return rc;
+    ProfScope ps(ctx, p == 0 ? PDP_STAGE_ONESWEEP_FIRST : PDP_STAGE_ONESWEEP_REST, stream);
+    if (p == 0)
+      hipLaunchKernelGGL(k_onesweep<true>, dim3((unsigned)L.tiles), dim3(kThreads), 0, stream, cols->pid, cols->pk,
+                         cols->value, (const Rec*)nullptr, dst, n, counters, (int)kCtrNKept, ks, p, off + p * kHist,
+                         status, ctx->epoch, counters, (int)kCtrTile0 + p);
+    else
+      hipLaunchKernelGGL(k_onesweep<false>, dim3((unsigned)L.tiles), dim3(kThreads), 0, stream,
+                         (const int64_t*)nullptr, (const int64_t*)nullptr, (const double*)nullptr, src, dst, n,
+                         counters, (int)kCtrNKept, ks, p, off + p * kHist, status, ctx->epoch, counters,
+                         (int)kCtrTile0 + p);
+    src = dst;
+    dst = (dst == recs_a) ? recs_b : recs_a;
+  }
+  HIP_TRY(hipGetLastError());
+  Rec* sorted = src;
+  Rec* spare = dst;
+
+  OvList ov{ranges, counters};
+  const int64_t seg_grid = (n + kSegCap - 1) / kSegCap;
+  {
+    ProfScope ps(ctx, PDP_STAGE_BUCKETS, stream);
+    hipLaunchKernelGGL(k_buckets, dim3((unsigned)seg_grid), dim3(kThreads), 0, stream, sorted, counters,
+                       (int)kCtrNKept, sp, acc, ov, (int)bp->debug_force_fallback);
+  }
+  HIP_TRY(hipGetLastError());
+
+  unsigned long long host_ctr[8];
+  HIP_TRY(hipMemcpyAsync(host_ctr, counters, sizeof(host_ctr), hipMemcpyDeviceToHost, stream));
+  HIP_TRY(hipStreamSynchronize(stream));
+  ctx->stats.kept_rows_in = (int64_t)host_ctr[kCtrNKept];
+  if (host_ctr[kCtrErr]) return fail(PDP_ERR_INTERNAL, "radix look-back timed out");
+  if (host_ctr[kCtrInvalid]) return fail(PDP_ERR_OUT_OF_RANGE, "privacy id or partition id out of range");
+  std::vector<unsigned long long> rg;
+  if (host_ctr[kCtrFull]) {
+    // Too many overflowing buckets: redo everything on the generic path.
+    HIP_TRY(hipMemsetAsync(acc.row_count, 0, (size_t)P * 8, stream));
+    if (acc.count) HIP_TRY(hipMemsetAsync(acc.count, 0, (size_t)P * 8, stream));
+    if (acc.x) HIP_TRY(hipMemsetAsync(acc.x, 0, (size_t)P * 8, stream));
+    if (acc.y) HIP_TRY(hipMemsetAsync(acc.y, 0, (size_t)P * 8, stream));
+    rg = {0ull, host_ctr[kCtrNKept]};
+  } else if (host_ctr[kCtrNRanges]) {
+    rg.resize(2 * host_ctr[kCtrNRanges]);
+    HIP_TRY(hipMemcpyAsync(rg.data(), ranges, rg.size() * 8, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipStreamSynchronize(stream));
+  }
+  if (!rg.empty()) {
+    int rc = run_generic(ctx, sorted, spare, rg, plan, sp, bp, ks.num_pids, ks.num_parts, acc, hist, off, counters,
+                         status, status_bytes, workspace, stream);
+    if (rc) return rc;
+    unsigned long long err = 0;
+    HIP_TRY(hipMemcpyAsync(&err, counters + kCtrErr, 8, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipStreamSynchronize(stream));
+    if (err) return fail(PDP_ERR_INTERNAL, "radix look-back timed out (generic path)");
+  }
+  return 0;
+}
+
+int pdp_release(pdp_ctx* ctx, const pdp_accumulators* accp, int64_t P, int64_t pk_offset,
+                const pdp_release_params* rp, const pdp_outputs* out, void* stream_) {
+  if (!ctx || !accp || !rp || !out || !out->keep || !out->metrics) return fail(PDP_ERR_INVALID_ARG, "null argument");
+  if (P < 0) return fail(PDP_ERR_INVALID_ARG, "num_partitions < 0");
+  hipStream_t stream = (hipStream_t)stream_;
+  RelParams q{};
+  q.metrics = rp->metrics;
+  q.kind = rp->noise_kind;
+  q.selection = rp->selection;
+  q.add_noise = rp->add_noise;
+  q.seed = rp->noise_seed;
+  q.max_rows = rp->max_rows_per_privacy_id > 0 ? rp->max_rows_per_privacy_id : 1;
+  int32_t fields[5];
+  q.nfields = pdp_metric_fields(rp->metrics, fields);
+  for (int i = 0; i < q.nfields; ++i) q.field[i] = fields[i];
+  const double l0 = (double)rp->max_partitions_contributed, linf = (double)rp->max_contributions_per_partition;
+  const int kind = rp->noise_kind;
+  const int m = rp->metrics;
+  if (kind != PDP_NOISE_LAPLACE && kind != PDP_NOISE_GAUSSIAN)
+    return fail(PDP_ERR_INVALID_ARG, "Noise kind must be either Laplace or Gaussian.");
+  auto need = [&](int mech) -> int {
+    if (!(rp->eps[mech] > 0)) return fail(PDP_ERR_INVALID_ARG, "mechanism epsilon must be positive");
+    if (kind == PDP_NOISE_GAUSSIAN && !(rp->delta[mech] > 0))
+      return fail(PDP_ERR_INVALID_ARG, "Gaussian mechanism needs delta > 0");
+    return 0;
+  };
+  const double a = rp->min_value, b = rp->max_value;
+  q.a = a;
+  q.mid = a + (b - a) / 2;
+  if (m & (PDP_METRIC_VARIANCE | PDP_METRIC_MEAN)) {
+    if (!rp->has_value_bounds) return fail(PDP_ERR_INVALID_ARG, "MEAN/VARIANCE need min_value/max_value");
+    const bool var = (m & PDP_METRIC_VARIANCE) != 0;
+    const int mech = var ? PDP_MECH_VARIANCE : PDP_MECH_MEAN;
+    if (int rc = need(mech)) return rc;
+    const int parts = var ? 3 : 2;
+    // equally_split_budget, dp_computations.py:224-252
+    const double e = rp->eps[mech], d = rp->delta[mech];
+    double eu = 0, du = 0, be[3], bd[3];
+    for (int i = 0; i < parts - 1; ++i) {
+      be[i] = e / parts;
+      bd[i] = d / parts;
+      eu += be[i];
+      du += bd[i];
+    }
+    be[parts - 1] = e - eu;
+    bd[parts - 1] = d - du;
+    q.s_mean_count = noise_scale(kind, be[0], bd[0], l0, linf);
+    q.mean_degenerate = (a == b);
+    q.s_mean_nsum = q.mean_degenerate ? 0.0 : noise_scale(kind, be[1], bd[1], l0, linf * std::fabs(q.mid - a));
+    if (var) {
+      double sa, sb;  // compute_squares_interval, dp_computations.py:58-62
+      if (a < 0 && 0 < b) {
+        sa = 0;
+        sb = std::max(a * a, b * b);
+      } else {
+        sa = a * a;
+        sb = b * b;
+      }
+      q.sq_a = sa;
+      q.sq_degenerate = (sa == sb);
+      q.sq_mid = sa + (sb - sa) / 2;
+      q.s_var_nsq = q.sq_degenerate ? 0.0 : noise_scale(kind, be[2], bd[2], l0, linf * std::fabs(q.sq_mid - sa));
+    }
+  } else {
+    if (m & PDP_METRIC_COUNT) {
+      if (int rc = need(PDP_MECH_COUNT)) return rc;
+      q.s_count = noise_scale(kind, rp->eps[PDP_MECH_COUNT], rp->delta[PDP_MECH_COUNT], l0, linf);
+    }
+    if (m & PDP_METRIC_SUM) {
+      double slinf;
+      if (rp->has_value_bounds)
+        slinf = linf * std::max(std::fabs(a), std::fabs(b));
+      else if (rp->has_partition_bounds)
+        slinf = std::max(std::fabs(rp->min_sum_per_partition), std::fabs(rp->max_sum_per_partition));
+      else
+        return fail(PDP_ERR_INVALID_ARG, "SUM needs value or partition bounds");
+      q.sum_zero = (slinf == 0.0);
+      if (!q.sum_zero) {
+        if (int rc = need(PDP_MECH_SUM)) return rc;
+        q.s_sum = noise_scale(kind, rp->eps[PDP_MECH_SUM], rp->delta[PDP_MECH_SUM], l0, slinf);
+      }
+    }
+  }
+  if (m & PDP_METRIC_PRIVACY_ID_COUNT) {
+    if (int rc = need(PDP_MECH_PRIVACY_ID_COUNT)) return rc;
+    q.s_pid = noise_scale(kind, rp->eps[PDP_MECH_PRIVACY_ID_COUNT], rp->delta[PDP_MECH_PRIVACY_ID_COUNT], l0, linf);
+  }
+  if (rp->selection != PDP_SELECTION_NONE) {
+    const double se = rp->eps[PDP_MECH_SELECTION], sd = rp->delta[PDP_MECH_SELECTION];
+    if (rp->selection == PDP_SELECTION_TRUNCATED_GEOMETRIC) {
+      if (!(ctx->table_key[0] == se && ctx->table_key[1] == sd && ctx->table_key[2] == l0 && ctx->table_dev)) {
+        int64_t len = 0;
+        if (int rc = pdp_truncated_geometric_table(se, sd, rp->max_partitions_contributed, nullptr, 0, &len)) return rc;
+        ctx->table_host.assign((size_t)len, 0.0);
+        int64_t len2 = 0;
+        pdp_truncated_geometric_table(se, sd, rp->max_partitions_contributed, ctx->table_host.data(), len, &len2);
+        if ((size_t)len > ctx->table_cap) {
+          if (ctx->table_dev) HIP_TRY(hipFree(ctx->table_dev));
+          ctx->table_dev = nullptr;
+          HIP_TRY(hipMalloc((void**)&ctx->table_dev, (size_t)len * 8));
+          ctx->table_cap = (size_t)len;
+        }
+        HIP_TRY(hipMemcpyAsync(ctx->table_dev, ctx->table_host.data(), (size_t)len * 8, hipMemcpyHostToDevice, stream));
+        HIP_TRY(hipStreamSynchronize(stream));
+        ctx->table_len = len;
+        ctx->table_key[0] = se;
+        ctx->table_key[1] = sd;
+        ctx->table_key[2] = l0;
+      }
+      q.table = ctx->table_dev;
+      q.tlen = ctx->table_len;
+    } else if (rp->selection == PDP_SELECTION_LAPLACE_THRESHOLDING ||
+               rp->selection == PDP_SELECTION_GAUSSIAN_THRESHOLDING) {
+      if (int rc = pdp_selection_threshold(rp->selection, se, sd, rp->max_partitions_contributed, &q.sel_thr,
+                                           &q.sel_scale))
+        return rc;
+    } else {
+      return fail(PDP_ERR_INVALID_ARG, "Unknown partition selection strategy");
+    }
+  }
+  if (P == 0) return 0;
+  ProfScope ps(ctx, PDP_STAGE_RELEASE, stream);
+  hipLaunchKernelGGL(k_release, dim3(grid_for(P, kThreads, 8192)), dim3(kThreads), 0, stream,
+                     (const unsigned long long*)accp->row_count, (const unsigned long long*)accp->count, accp->x,
+                     accp->y, P, pk_offset, q, out->keep, out->metrics);
+  HIP_TRY(hipGetLastError());
+  return 0;
+}
+
+int pdp_profile_enable(pdp_ctx* ctx, int enable) {
+  if (!ctx) return fail(PDP_ERR_INVALID_ARG, "null ctx");
+  ctx->prof = enable != 0;
+  return 0;
+}
+
+int pdp_profile_read(pdp_ctx* ctx, double* ms_out, int64_t* launches_out, int reset) {
+  if (!ctx) return fail(PDP_ERR_INVALID_ARG, "null ctx");
+  for (auto& r : ctx->pending) {
+    HIP_TRY(hipEventSynchronize(r.b));
+    float ms = 0.f;
+    HIP_TRY(hipEventElapsedTime(&ms, r.a, r.b));
+    ctx->prof_ms[r.stage] += ms;
+    ctx->prof_n[r.stage] += 1;
+    ctx->pool.push_back(r.a);
+    ctx->pool.push_back(r.b);
+  }
+  ctx->pending.clear();
+  for (int i = 0; i < PDP_NUM_STAGES; ++i) {
+    if (ms_out) ms_out[i] = ctx->prof_ms[i];
+    if (launches_out) launches_out[i] = ctx->prof_n[i];
+    if (reset) {
+      ctx->prof_ms[i] = 0;
+      ctx->prof_n[i] = 0;
+    }
+  }
+  return 0;
+}
+
+int pdp_generate_synthetic(int64_t* pid, int64_t* pk, double* value, int64_t n, int64_t row_offset, int64_t U,
+                           int64_t P, double zipf_s, int32_t value_kind, double lo, double hi, uint64_t seed,
+                           void* stream) {
+  if (n < 0 || U < 1 || P < 1 || !pid || !pk) return fail(PDP_ERR_INVALID_ARG, "bad generator args");
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(k_generate, dim3(grid_for(n, kThreads, 16384)), dim3(kThreads), 0, (hipStream_t)stream, pid, pk,
+                     value, n, row_offset, U, P, zipf_s, value_kind, lo, hi, seed);
+  HIP_TRY(hipGetLastError());
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,123 @@
+"""Multi-GPU execution: one process per GPU, rows sharded by privacy id.
+
+Bounding is per privacy id, so once every row of a privacy id lives on one
+rank (rank = shard_of(pid)), contribution bounding is rank-local
+(contribution_bounders.py:87-92 groups by pid).  Each rank reduces its rows
+to dense per-partition accumulators over all P partitions; one reduce-scatter
+per accumulator array (int64 counts stay exact, fp64 sums differ only in
+summation order) leaves rank r with the sums of partition block
+[r*B, (r+1)*B); selection and noise run once there.  Philox counters use the
+global partition id, so released values do not depend on the rank count.
+
+The collective backend is whatever ``torch.distributed`` was initialised
+with: ``nccl`` (= RCCL over xGMI on MI355X) for GPUs, ``gloo`` in CPU tests.
+"""
+import dataclasses
+from typing import Optional
+
+PID_SHARD_SALT = 0x9E3779B97F4A7C15
+
+
+def shard_of(pid, world_size: int):
+    """Rank owning a (dense) privacy id: splitmix64(pid ^ salt) % world_size
+    (numpy / torch int64 arrays or ints)."""
+    import numpy as np
+    x = np.asarray(pid, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        z = x ^ np.uint64(PID_SHARD_SALT)
+        z = z + np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z = z ^ (z >> np.uint64(31))
+    return (z % np.uint64(world_size)).astype(np.int64)
+
+
+@dataclasses.dataclass
+class World:
+    """Process group view: ``rank``/``size`` and the torch.distributed group."""
+    rank: int
+    size: int
+    group: Optional[object] = None
+
+    @classmethod
+    def from_env(cls, backend: Optional[str] = None):
+        import os
+        import torch.distributed as dist
+        if not dist.is_initialized():
+            dist.init_process_group(backend=backend or ("nccl" if _has_gpu() else "gloo"))
+        return cls(dist.get_rank(), dist.get_world_size(), None)
+
+    def block(self, num_partitions: int):
+        """Partition block owned by this rank: (offset, length, padded P)."""
+        b = (num_partitions + self.size - 1) // self.size
+        off = min(self.rank * b, num_partitions)
+        return off, max(0, min(b, num_partitions - off)), b * self.size
+
+    def reduce_scatter_accumulators(self, acc, num_partitions: int):
+        """Sums per-rank dense accumulators; returns owned-block tensors
+        [row_count, count, x, y] (None where absent)."""
+        import torch
+        import torch.distributed as dist
+        _, _, padded = self.block(num_partitions)
+        b = padded // self.size
+        outs = []
+        for t in (acc.row_count, acc.count, acc.x, acc.y):
+            if t is None:
+                outs.append(None)
+                continue
+            src = t[:num_partitions]
+            if padded != num_partitions:
+                src = torch.cat([src, src.new_zeros(padded - num_partitions)])
+            dst = src.new_empty(b)
+            dist.reduce_scatter_tensor(dst, src.contiguous(), op=dist.ReduceOp.SUM, group=self.group)
+            outs.append(dst)
+        return outs
+
+    def aggregate(self, ex, pid, pk, value, num_privacy_ids, num_partitions, bounds, rel, gather=True):
+        """Rank-local bound+accumulate, reduce-scatter, owner-side release.
+
+        Returns (keep [P], metrics [F, P], fields) of ALL partitions on every
+        rank when ``gather`` (all-gather of the owned blocks), else of the
+        owned block only."""
+        import torch
+        import torch.distributed as dist
+        acc = ex.accumulate(pid, pk, value, num_privacy_ids, num_partitions, bounds)
+        off, length, padded = self.block(num_partitions)
+        owned = self.reduce_scatter_accumulators(acc, num_partitions)
+        block_acc = _BlockAcc(owned, padded // self.size)
+        keep, out, fields = ex.release(block_acc, rel, bounds, pk_offset=off, num_partitions=padded // self.size)
+        if not gather:
+            return keep[:length], out[:, :length], fields
+        b = padded // self.size
+        keep_all = keep.new_empty(padded)
+        dist.all_gather_into_tensor(keep_all, keep.contiguous()[:b], group=self.group)
+        f = out.shape[0]
+        out_all = out.new_empty((self.size, f, b))
+        dist.all_gather_into_tensor(out_all, out.contiguous(), group=self.group)
+        out_all = out_all.permute(1, 0, 2).reshape(f, padded)
+        return keep_all[:num_partitions], out_all[:, :num_partitions], fields
+
+
+class _BlockAcc:
+    """Accumulators view of the owned block (duck-types executor.Accumulators)."""
+
+    def __init__(self, tensors, num_partitions):
+        self.row_count, self.count, self.x, self.y = tensors
+        self.num_partitions = num_partitions
+
+    def as_struct(self, offset: int = 0):
+        import ctypes
+        from . import native
+
+        def p(t):
+            return ctypes.c_void_p(t.data_ptr() + 8 * offset) if t is not None else None
+
+        return native.Accumulators(p(self.row_count), p(self.count), p(self.x), p(self.y))
+
+
+def _has_gpu():
+    try:
+        import torch
+        return torch.cuda.is_available()
+    except Exception:
+        return False

@@ -1,0 +1,182 @@
+"""Device-side execution of the aggregate path through libpdp_hip.so.
+
+``HipExecutor`` owns one pdp_ctx, a cached device workspace and the stream
+it launches on (torch's current stream of the device).  Torch is used for
+device memory and streams only; all compute is in the HIP library.
+"""
+import ctypes
+import dataclasses
+import secrets
+from typing import Optional, Sequence
+
+from . import native
+
+
+@dataclasses.dataclass
+class BoundConfig:
+    """Bounding parameters (AggregateParams subset)."""
+    metrics_mask: int
+    max_partitions_contributed: int
+    max_contributions_per_partition: int
+    min_value: Optional[float] = None
+    max_value: Optional[float] = None
+    min_sum_per_partition: Optional[float] = None
+    max_sum_per_partition: Optional[float] = None
+    bounds_already_enforced: bool = False
+    sampling_seed: Optional[int] = None
+    debug_force_fallback: bool = False
+
+
+@dataclasses.dataclass
+class ReleaseConfig:
+    """Noise / selection parameters after compute_budgets()."""
+    metrics_mask: int
+    noise_kind: int
+    selection: int
+    eps: Sequence[float]
+    delta: Sequence[float]
+    max_rows_per_privacy_id: int = 1
+    add_noise: bool = True
+    noise_seed: Optional[int] = None
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+class Accumulators:
+    """Dense per-partition accumulators on the device."""
+
+    def __init__(self, torch, num_partitions: int, device, metrics_mask: int):
+        m = metrics_mask
+        i64, f64 = torch.int64, torch.float64
+        P = max(int(num_partitions), 1)
+        self.num_partitions = int(num_partitions)
+        self.row_count = torch.empty(P, dtype=i64, device=device)
+        need_count = bool(m & (native.METRIC_COUNT | native.METRIC_MEAN | native.METRIC_VARIANCE))
+        need_x = bool(m & (native.METRIC_SUM | native.METRIC_MEAN | native.METRIC_VARIANCE))
+        self.count = torch.empty(P, dtype=i64, device=device) if need_count else None
+        self.x = torch.empty(P, dtype=f64, device=device) if need_x else None
+        self.y = torch.empty(P, dtype=f64, device=device) if m & native.METRIC_VARIANCE else None
+
+    def tensors(self):
+        return [t for t in (self.row_count, self.count, self.x, self.y) if t is not None]
+
+    def as_struct(self, offset: int = 0) -> native.Accumulators:
+
+        def p(t):
+            return ctypes.c_void_p(t.data_ptr() + 8 * offset) if t is not None else None
+
+        return native.Accumulators(p(self.row_count), p(self.count), p(self.x), p(self.y))
+
+
+class HipExecutor:
+
+    def __init__(self, device=None):
+        import torch
+        if not torch.cuda.is_available():
+            raise native.NativeError("HipBackend needs a ROCm GPU (torch.cuda.is_available() is False); "
+                                     "the aggregate path has no CPU fallback.")
+        self.torch = torch
+        self.device = torch.device("cuda", torch.cuda.current_device() if device is None else device)
+        self.lib = native.lib()
+        self.ctx = self.lib.pdp_ctx_create(self.device.index)
+        self._ws = None
+
+    def __del__(self):
+        try:
+            if getattr(self, "ctx", None):
+                self.lib.pdp_ctx_destroy(self.ctx)
+        except Exception:
+            pass
+
+    @property
+    def stream_handle(self):
+        return ctypes.c_void_p(self.torch.cuda.current_stream(self.device).cuda_stream)
+
+    def _workspace(self, nbytes: int):
+        if self._ws is None or self._ws.numel() < nbytes:
+            self._ws = None
+            self._ws = self.torch.empty(max(nbytes, 256), dtype=self.torch.uint8, device=self.device)
+        return self._ws
+
+    def accumulate(self, pid, pk, value, num_privacy_ids: int, num_partitions: int, cfg: BoundConfig,
+                   acc: Optional[Accumulators] = None) -> Accumulators:
+        """pdp_bound_accumulate on int64 pid/pk and float64 value device tensors."""
+        torch = self.torch
+        n = int(pk.numel())
+        for t, dt in ((pid, torch.int64), (pk, torch.int64), (value, torch.float64)):
+            if t is not None:
+                assert t.device == self.device and t.dtype == dt and t.is_contiguous(), (t.device, t.dtype)
+                assert t.numel() == n
+        cols = native.Columns(_ptr(pid), _ptr(pk), _ptr(value), n, int(max(num_privacy_ids, 1)),
+                              int(num_partitions))
+        seed = cfg.sampling_seed if cfg.sampling_seed is not None else secrets.randbits(64)
+        bp = native.BoundParams(
+            cfg.metrics_mask, int(cfg.bounds_already_enforced), cfg.max_partitions_contributed,
+            cfg.max_contributions_per_partition, int(cfg.min_value is not None),
+            int(cfg.min_sum_per_partition is not None),
+            float(cfg.min_value or 0.0), float(cfg.max_value or 0.0),
+            float(cfg.min_sum_per_partition or 0.0), float(cfg.max_sum_per_partition or 0.0),
+            seed, int(cfg.debug_force_fallback), 0)
+        if acc is None:
+            acc = Accumulators(torch, num_partitions, self.device, cfg.metrics_mask)
+        nbytes = ctypes.c_size_t(0)
+        native.check(self.lib.pdp_workspace_size(ctypes.byref(cols), ctypes.byref(bp), ctypes.byref(nbytes)),
+                     "pdp_workspace_size")
+        ws = self._workspace(nbytes.value)
+        accs = acc.as_struct()
+        native.check(self.lib.pdp_bound_accumulate(self.ctx, ctypes.byref(cols), ctypes.byref(bp), ctypes.byref(accs),
+                                                   ctypes.c_void_p(ws.data_ptr()), ws.numel(), self.stream_handle),
+                     "pdp_bound_accumulate")
+        return acc
+
+    def release(self, acc: Accumulators, cfg: ReleaseConfig, bounds: BoundConfig, pk_offset: int = 0,
+                num_partitions: Optional[int] = None, offset_in_acc: int = 0):
+        """pdp_release -> (keep uint8 [P], metrics float64 [F, P], field names)."""
+        torch = self.torch
+        P = acc.num_partitions if num_partitions is None else int(num_partitions)
+        fields = native.metric_fields(cfg.metrics_mask)
+        keep = torch.empty(max(P, 1), dtype=torch.uint8, device=self.device)
+        out = torch.empty((max(len(fields), 1), max(P, 1)), dtype=torch.float64, device=self.device)
+        eps = (ctypes.c_double * native.NUM_MECH)(*cfg.eps)
+        delta = (ctypes.c_double * native.NUM_MECH)(*cfg.delta)
+        seed = cfg.noise_seed if cfg.noise_seed is not None else secrets.randbits(64)
+        rp = native.ReleaseParams(
+            cfg.metrics_mask, cfg.noise_kind, cfg.selection, int(cfg.add_noise), bounds.max_partitions_contributed,
+            bounds.max_contributions_per_partition, int(bounds.min_value is not None),
+            int(bounds.min_sum_per_partition is not None), float(bounds.min_value or 0.0),
+            float(bounds.max_value or 0.0), float(bounds.min_sum_per_partition or 0.0),
+            float(bounds.max_sum_per_partition or 0.0), eps, delta, int(cfg.max_rows_per_privacy_id), seed)
+        outs = native.Outputs(ctypes.c_void_p(keep.data_ptr()), ctypes.c_void_p(out.data_ptr()))
+        accs = acc.as_struct(offset_in_acc)
+        native.check(self.lib.pdp_release(self.ctx, ctypes.byref(accs), P, int(pk_offset), ctypes.byref(rp),
+                                          ctypes.byref(outs), self.stream_handle), "pdp_release")
+        return keep[:P], out[:, :P], fields
+
+    def profile(self, enable: bool = True):
+        native.check(self.lib.pdp_profile_enable(self.ctx, int(enable)), "pdp_profile_enable")
+
+    def profile_read(self, reset: bool = True):
+        """-> {stage: (total ms, launches)} of the recorded kernels."""
+        n = len(native.STAGES)
+        ms = (ctypes.c_double * n)()
+        cnt = (ctypes.c_int64 * n)()
+        native.check(self.lib.pdp_profile_read(self.ctx, ms, cnt, int(reset)), "pdp_profile_read")
+        return {s: (ms[i], cnt[i]) for i, s in enumerate(native.STAGES)}
+
+    def stats(self) -> native.Stats:
+        s = native.Stats()
+        native.check(self.lib.pdp_get_stats(self.ctx, ctypes.byref(s)), "pdp_get_stats")
+        return s
+
+    def generate(self, n: int, num_privacy_ids: int, num_partitions: int, seed: int, zipf_s: float = 0.0,
+                 value_kind: int = 0, lo: float = 0.0, hi: float = 10.0, row_offset: int = 0, with_value=True):
+        torch = self.torch
+        pid = torch.empty(max(n, 1), dtype=torch.int64, device=self.device)[:n]
+        pk = torch.empty(max(n, 1), dtype=torch.int64, device=self.device)[:n]
+        val = torch.empty(max(n, 1), dtype=torch.float64, device=self.device)[:n] if with_value else None
+        native.check(self.lib.pdp_generate_synthetic(_ptr(pid), _ptr(pk), _ptr(val), n, row_offset, num_privacy_ids,
+                                                     num_partitions, zipf_s, value_kind, lo, hi, seed,
+                                                     self.stream_handle), "pdp_generate_synthetic")
+        return pid, pk, val

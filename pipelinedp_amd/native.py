@@ -1,0 +1,141 @@
+"""ctypes binding of libpdp_hip.so (C ABI: include/pdp_hip.h).
+
+The library is built in-tree by ``pipelinedp_amd/build.py`` (hipcc,
+--offload-arch=gfx950).  There is no CPU fallback: if the library is missing
+every call raises.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libpdp_hip.so")
+
+PDP_OK = 0
+METRIC_COUNT, METRIC_SUM, METRIC_MEAN, METRIC_VARIANCE, METRIC_PRIVACY_ID_COUNT = 1, 2, 4, 8, 16
+FIELD_NAMES = {0: "variance", 1: "mean", 2: "count", 3: "sum", 4: "privacy_id_count"}
+NOISE_LAPLACE, NOISE_GAUSSIAN = 0, 1
+SELECTION_NONE, SELECTION_TRUNCATED_GEOMETRIC, SELECTION_LAPLACE, SELECTION_GAUSSIAN = 0, 1, 2, 3
+MECH_COUNT, MECH_SUM, MECH_MEAN, MECH_VARIANCE, MECH_PRIVACY_ID_COUNT, MECH_SELECTION = range(6)
+NUM_MECH = 6
+
+c_i32, c_i64, c_u64, c_f64 = ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64, ctypes.c_double
+c_vp = ctypes.c_void_p
+
+
+class Columns(ctypes.Structure):
+    _fields_ = [("pid", c_vp), ("pk", c_vp), ("value", c_vp), ("num_rows", c_i64),
+                ("num_privacy_ids", c_i64), ("num_partitions", c_i64)]
+
+
+class BoundParams(ctypes.Structure):
+    _fields_ = [("metrics", c_i32), ("bounds_already_enforced", c_i32),
+                ("max_partitions_contributed", c_i64), ("max_contributions_per_partition", c_i64),
+                ("has_value_bounds", c_i32), ("has_partition_bounds", c_i32),
+                ("min_value", c_f64), ("max_value", c_f64),
+                ("min_sum_per_partition", c_f64), ("max_sum_per_partition", c_f64),
+                ("sampling_seed", c_u64), ("debug_force_fallback", c_i32), ("reserved", c_i32)]
+
+
+class Accumulators(ctypes.Structure):
+    _fields_ = [("row_count", c_vp), ("count", c_vp), ("x", c_vp), ("y", c_vp)]
+
+
+class ReleaseParams(ctypes.Structure):
+    _fields_ = [("metrics", c_i32), ("noise_kind", c_i32), ("selection", c_i32), ("add_noise", c_i32),
+                ("max_partitions_contributed", c_i64), ("max_contributions_per_partition", c_i64),
+                ("has_value_bounds", c_i32), ("has_partition_bounds", c_i32),
+                ("min_value", c_f64), ("max_value", c_f64),
+                ("min_sum_per_partition", c_f64), ("max_sum_per_partition", c_f64),
+                ("eps", c_f64 * NUM_MECH), ("delta", c_f64 * NUM_MECH),
+                ("max_rows_per_privacy_id", c_i64), ("noise_seed", c_u64)]
+
+
+class Outputs(ctypes.Structure):
+    _fields_ = [("keep", c_vp), ("metrics", c_vp)]
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [("kept_rows_in", c_i64), ("fallback_rows", c_i64), ("fallback_ranges", c_i64),
+                ("sort_passes", c_i32), ("bucket_low_bits", c_i32)]
+
+
+# Every symbol declared in include/pdp_hip.h: (name, restype, argtypes).
+SIGNATURES = [
+    ("pdp_abi_version", c_i32, []),
+    ("pdp_last_error", ctypes.c_char_p, []),
+    ("pdp_ctx_create", c_vp, [c_i32]),
+    ("pdp_ctx_destroy", None, [c_vp]),
+    ("pdp_workspace_size", c_i32, [ctypes.POINTER(Columns), ctypes.POINTER(BoundParams),
+                                   ctypes.POINTER(ctypes.c_size_t)]),
+    ("pdp_bound_accumulate", c_i32, [c_vp, ctypes.POINTER(Columns), ctypes.POINTER(BoundParams),
+                                     ctypes.POINTER(Accumulators), c_vp, ctypes.c_size_t, c_vp]),
+    ("pdp_release", c_i32, [c_vp, ctypes.POINTER(Accumulators), c_i64, c_i64, ctypes.POINTER(ReleaseParams),
+                            ctypes.POINTER(Outputs), c_vp]),
+    ("pdp_metric_fields", c_i32, [c_i32, ctypes.POINTER(c_i32)]),
+    ("pdp_gaussian_sigma", c_f64, [c_f64, c_f64, c_f64]),
+    ("pdp_truncated_geometric_table", c_i32, [c_f64, c_f64, c_i64, ctypes.POINTER(c_f64), c_i64,
+                                              ctypes.POINTER(c_i64)]),
+    ("pdp_selection_threshold", c_i32, [c_i32, c_f64, c_f64, c_i64, ctypes.POINTER(c_f64),
+                                        ctypes.POINTER(c_f64)]),
+    ("pdp_generate_synthetic", c_i32, [c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_f64, c_i32, c_f64,
+                                       c_f64, c_u64, c_vp]),
+    ("pdp_get_stats", c_i32, [c_vp, ctypes.POINTER(Stats)]),
+    ("pdp_profile_enable", c_i32, [c_vp, c_i32]),
+    ("pdp_profile_read", c_i32, [c_vp, ctypes.POINTER(c_f64), ctypes.POINTER(c_i64), c_i32]),
+]
+
+STAGES = ["histogram", "onesweep_first", "onesweep_rest", "buckets", "generic", "release", "enforced"]
+
+_lib = None
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load libpdp_hip.so (fails loudly when it has not been built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise NativeError(f"{LIB_PATH} is missing: build it with `python -m pipelinedp_amd.build` "
+                              "(hipcc --offload-arch=gfx950); there is no CPU fallback.")
+        handle = ctypes.CDLL(LIB_PATH)
+        for name, res, args in SIGNATURES:
+            fn = getattr(handle, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = handle
+    return _lib
+
+
+def check(rc: int, what: str) -> None:
+    if rc != PDP_OK:
+        msg = lib().pdp_last_error()
+        raise NativeError(f"{what} failed ({rc}): {msg.decode() if msg else ''}")
+
+
+def metric_fields(mask: int):
+    buf = (c_i32 * 5)()
+    n = lib().pdp_metric_fields(mask, buf)
+    return [FIELD_NAMES[buf[i]] for i in range(n)]
+
+
+def gaussian_sigma(eps: float, delta: float, l2: float) -> float:
+    return lib().pdp_gaussian_sigma(eps, delta, l2)
+
+
+def truncated_geometric_table(eps: float, delta: float, k: int):
+    n = c_i64(0)
+    check(lib().pdp_truncated_geometric_table(eps, delta, k, None, 0, ctypes.byref(n)), "table size")
+    buf = (c_f64 * n.value)()
+    n2 = c_i64(0)
+    check(lib().pdp_truncated_geometric_table(eps, delta, k, buf, n.value, ctypes.byref(n2)), "table")
+    return list(buf)
+
+
+def selection_threshold(selection: int, eps: float, delta: float, k: int):
+    thr, scale = c_f64(0), c_f64(0)
+    check(lib().pdp_selection_threshold(selection, eps, delta, k, ctypes.byref(thr), ctypes.byref(scale)),
+          "selection threshold")
+    return thr.value, scale.value

@@ -1,0 +1,308 @@
+"""GPU parity: the HIP path (through the C ABI) against the CPU oracle and the
+reference golden vectors.
+
+Tolerances: counts / privacy-id counts / keep decisions bit-exact; fp64 sums
+|gpu - oracle| <= 1e-9 * (sum of |terms| + 1) (summation order differs);
+noisy outputs with identical Philox draws rel 1e-9 (libm ulps).
+"""
+import math
+
+import numpy as np
+import pytest
+
+import pdp_oracle as o
+from golden_util import aggregate_cases, encode_case, load
+
+pytestmark = pytest.mark.gpu
+
+MASK = {"count": 1, "sum": 2, "mean": 4, "variance": 8, "privacy_id_count": 16}
+
+
+@pytest.fixture(scope="module")
+def ex():
+    from pipelinedp_amd.executor import HipExecutor
+    return HipExecutor(0)
+
+
+def _dev(a, torch):
+    return None if a is None else torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+def run_gpu(ex, pid, pk, val, U, P, bp: o.BoundParams, mask, seed=3, fallback=False):
+    import torch
+    from pipelinedp_amd.executor import BoundConfig
+    cfg = BoundConfig(mask, bp.max_partitions_contributed, bp.max_contributions_per_partition, bp.min_value,
+                      bp.max_value, bp.min_sum_per_partition, bp.max_sum_per_partition,
+                      bp.contribution_bounds_already_enforced, seed, fallback)
+    acc = ex.accumulate(_dev(pid, torch), _dev(pk, torch), _dev(val, torch), U, P, cfg)
+    torch.cuda.synchronize()
+    g = lambda t: None if t is None else t.cpu().numpy()  # noqa: E731
+    return cfg, acc, g(acc.row_count), g(acc.count), g(acc.x), g(acc.y)
+
+
+def check_acc(ref, rc, cnt, x, y, mask, value=None):
+    np.testing.assert_array_equal(rc, ref.row_count)
+    if cnt is not None:
+        np.testing.assert_array_equal(cnt, ref.count)
+    scale = 1e-9 * ((ref.count + 1) * (1.0 if value is None else max(1.0, float(np.abs(value).max())))**2) + 1e-9
+    if mask & (4 | 8):
+        assert np.all(np.abs(x - ref.nsum) <= scale)
+        if mask & 8:
+            assert np.all(np.abs(y - ref.nsumsq) <= scale)
+    elif mask & 2:
+        assert np.all(np.abs(x - ref.sum) <= scale)
+
+
+CONFIGS = [
+    # n, U, P, zipf, L0, Linf, vb, pb, mask
+    (30000, 500, 200, 1.1, 3, 2, (0.0, 10.0), None, 1 | 2 | 4),
+    (30000, 50, 1000, 0.0, 4, 1, (0.0, 10.0), None, 1 | 2 | 16),
+    (50000, 4000, 3000, 1.3, 2, 3, (-2.0, 7.0), None, 1 | 2 | 4 | 8),
+    (20000, 300, 100, 0.0, 5, 2, None, (-5.0, 40.0), 1 | 2),
+    (20000, 20, 50, 0.0, 60, 60, None, None, 1 | 16),  # non-binding, big pid buckets
+    (25000, 3, 7, 0.0, 2, 5, (1.0, 5.0), None, 1 | 2 | 4 | 16),  # pids with > 2048 rows -> generic path
+    (5000, 5000, 1, 0.0, 1, 1, (0.0, 1.0), None, 1 | 2),  # one partition
+    (4000, 1, 3000, 1.1, 7, 2, (0.0, 10.0), None, 1 | 4 | 16),  # one privacy id
+]
+
+
+@pytest.mark.parametrize("fallback", [False, True])
+@pytest.mark.parametrize("cfgi", range(len(CONFIGS)))
+def test_bound_accumulate_matches_oracle(ex, cfgi, fallback):
+    n, U, P, z, L0, Linf, vb, pb, mask = CONFIGS[cfgi]
+    pid, pk, val = o.synth_rows(n, U, P, seed=100 + cfgi, zipf_s=z, value_lo=-5, value_hi=15)
+    bp = o.BoundParams(L0, Linf, *(vb or (None, None)), *(pb or (None, None)))
+    need_val = bool(mask & (2 | 4 | 8))
+    _, _, rc, cnt, x, y = run_gpu(ex, pid, pk, val if need_val else None, U, P, bp, mask, seed=77 + cfgi,
+                                  fallback=fallback)
+    ref = o.bound_and_accumulate(pid, pk, val if need_val else None, P, bp, "feistel", seed=77 + cfgi)
+    check_acc(ref, rc, cnt, x, y, mask, val)
+    if cfgi == 5 and not fallback:
+        assert ex.stats().fallback_rows > 0  # huge privacy ids went through the generic path
+
+
+def test_dropped_rows_and_public_partitions(ex):
+    n, U, P = 20000, 800, 400
+    pid, pk, val = o.synth_rows(n, U, P, seed=9)
+    pk = np.where(pk % 3 == 0, -1, pk)  # non-public rows dropped
+    bp = o.BoundParams(3, 2, 0.0, 10.0)
+    _, _, rc, cnt, x, _ = run_gpu(ex, pid, pk, val, U, P, bp, 1 | 2 | 16)
+    ref = o.bound_and_accumulate(pid, pk, val, P, bp, "feistel", seed=3)
+    check_acc(ref, rc, cnt, x, None, 1 | 2 | 16, val)
+    assert rc[::3].sum() == 0
+    pk_all = np.full(n, -1)
+    _, _, rc, cnt, x, _ = run_gpu(ex, pid, pk_all, val, U, P, bp, 1 | 2)
+    assert rc.sum() == 0 and cnt.sum() == 0 and np.all(x == 0)
+
+
+def test_empty_input(ex):
+    bp = o.BoundParams(1, 1, 0.0, 1.0)
+    e = np.zeros(0, np.int64)
+    _, _, rc, cnt, x, _ = run_gpu(ex, e, e, np.zeros(0), 1, 5, bp, 1 | 2)
+    assert rc.sum() == 0 and cnt.sum() == 0
+
+
+def test_out_of_range_ids_raise(ex):
+    from pipelinedp_amd.native import NativeError
+    bp = o.BoundParams(1, 1, 0.0, 1.0)
+    pid = np.array([0, 1, 2], np.int64)
+    pk = np.array([0, 5, 1], np.int64)
+    with pytest.raises(NativeError, match="out of range"):
+        run_gpu(ex, pid, pk, np.zeros(3), 3, 5, bp, 1)
+
+
+def test_already_enforced_matches_oracle(ex):
+    n, P = 30000, 500
+    _, pk, val = o.synth_rows(n, 10, P, seed=4, zipf_s=1.2)
+    bp = o.BoundParams(3, 2, 0.0, 10.0, contribution_bounds_already_enforced=True)
+    _, _, rc, cnt, x, _ = run_gpu(ex, None, pk, val, 1, P, bp, 1 | 2)
+    ref = o.bound_and_accumulate(None, pk, val, P, bp)
+    check_acc(ref, rc, cnt, x, None, 1 | 2, val)
+
+
+def test_determinism_of_counts(ex):
+    n, U, P = 200000, 5000, 2000
+    pid, pk, val = o.synth_rows(n, U, P, seed=21, zipf_s=1.1)
+    bp = o.BoundParams(4, 2, 0.0, 10.0)
+    r1 = run_gpu(ex, pid, pk, val, U, P, bp, 1 | 4, seed=5)
+    r2 = run_gpu(ex, pid, pk, val, U, P, bp, 1 | 4, seed=5)
+    np.testing.assert_array_equal(r1[2], r2[2])
+    np.testing.assert_array_equal(r1[3], r2[3])
+    np.testing.assert_allclose(r1[4], r2[4], rtol=1e-12, atol=1e-9)
+
+
+# ---------------------------------------------------------------------------
+# Release (selection + noise) against the oracle with the same Philox draws
+# ---------------------------------------------------------------------------
+
+RELEASES = [
+    (("mean", "count", "sum", "privacy_id_count"), "laplace", "truncated_geometric"),
+    (("variance", "mean", "count", "sum"), "gaussian", "truncated_geometric"),
+    (("count", "sum"), "laplace", "laplace"),
+    (("count", "privacy_id_count"), "gaussian", "gaussian"),
+    (("sum",), "laplace", None),
+    (("mean",), "gaussian", None),
+]
+
+
+@pytest.mark.parametrize("ri", range(len(RELEASES)))
+def test_release_matches_oracle(ex, ri):
+    import torch
+    from pipelinedp_amd import native
+    from pipelinedp_amd.executor import ReleaseConfig
+    metrics, kind, sel = RELEASES[ri]
+    mask = sum(MASK[m] for m in metrics)
+    n, U, P = 60000, 3000, 1500
+    pid, pk, val = o.synth_rows(n, U, P, seed=31 + ri, zipf_s=1.1)
+    bp = o.BoundParams(3, 2, -1.0, 6.0)
+    cfg, acc, *_ = run_gpu(ex, pid, pk, val, U, P, bp, mask, seed=8)
+    ref = o.bound_and_accumulate(pid, pk, val, P, bp, "feistel", seed=8)
+    budgets = {m: (0.3 + 0.1 * i, 1e-7 * (i + 1)) for i, m in enumerate(("count", "sum", "mean", "variance",
+                                                                         "privacy_id_count"))}
+    slot = {"count": 0, "sum": 1, "mean": 2, "variance": 3, "privacy_id_count": 4}
+    eps = [0.0] * 6
+    delta = [0.0] * 6
+    for m, (e, d) in budgets.items():
+        eps[slot[m]], delta[slot[m]] = e, d
+    eps[5], delta[5] = 0.7, 1e-5
+    selc = {None: 0, "truncated_geometric": 1, "laplace": 2, "gaussian": 3}[sel]
+    rel = ReleaseConfig(mask, 0 if kind == "laplace" else 1, selc, eps, delta, 1, True, noise_seed=99 + ri)
+    keep, out, fields = ex.release(acc, rel, cfg)
+    torch.cuda.synchronize()
+    spec = o.ReleaseSpec(metrics, kind, budgets, sel, (0.7, 1e-5), 1)
+    k2, o2 = o.release(ref, bp, spec, seed=99 + ri)
+    assert fields == o.metric_field_order(metrics)
+    np.testing.assert_array_equal(keep.cpu().numpy().astype(bool), k2)
+    outn = out.cpu().numpy()
+    for i, f in enumerate(fields):
+        np.testing.assert_allclose(outn[i], o2[f], rtol=1e-9, atol=1e-7, err_msg=f)
+
+
+# ---------------------------------------------------------------------------
+# Full DPEngine API against the reference golden vectors (noise disabled)
+# ---------------------------------------------------------------------------
+
+
+@pytest.mark.parametrize("fallback", [False, True])
+@pytest.mark.parametrize("name", aggregate_cases())
+def test_engine_matches_reference_golden(name, fallback):
+    import pipelinedp_amd as pdp
+    from test_host_api import _params_from_cfg
+    d = load(name)
+    cfg = d["meta"]["cfg"]
+    acct = pdp.NaiveBudgetAccountant(total_epsilon=cfg.get("eps", 1.0), total_delta=cfg.get("delta", 1e-6))
+    backend = pdp.HipBackend(sampling_seed=1, noise_seed=2, _unsafe_disable_noise_for_testing=True,
+                             _debug_force_fallback=fallback)
+    engine = pdp.DPEngine(acct, backend)
+    enforced = cfg.get("already_enforced", False)
+    has_val = len(d["value"]) > 0
+    rows = list(zip(d["pid"].tolist() if len(d["pid"]) else [None] * len(d["pk"]), d["pk"].tolist(),
+                    d["value"].tolist() if has_val else [None] * len(d["pk"])))
+    ex = pdp.DataExtractors(privacy_id_extractor=None if enforced else (lambda r: r[0]),
+                            partition_extractor=lambda r: r[1], value_extractor=lambda r: r[2])
+    public = d["public"].tolist() if bool(d["has_public"]) else None
+    res = engine.aggregate(rows, _params_from_cfg(cfg), ex, public)
+    acct.compute_budgets()
+    got = dict(list(res))
+    exp_keys = d["out_keys"].tolist()
+    assert sorted(got) == sorted(exp_keys)
+    fields = d["meta"]["fields"]
+    vmax = float(np.abs(d["value"]).max()) if has_val else 1.0
+    for k, row in zip(exp_keys, d["out_vals"]):
+        t = got[k]
+        assert list(t._fields) == fields
+        for f, e in zip(fields, row):
+            g = getattr(t, f)
+            if f in ("count", "privacy_id_count"):
+                assert g == e, (k, f)
+            else:
+                n = max(getattr(t, "count", 1.0), 1.0) if "count" in fields else 1000.0
+                assert abs(g - e) <= 1e-9 * (n + 1) * max(vmax, 1.0)**2 + 1e-9, (k, f, g, e)
+
+
+def test_engine_columnar_device_input_and_select_partitions():
+    import torch
+    import pipelinedp_amd as pdp
+    n, U, P = 50000, 2000, 300
+    pid, pk, val = o.synth_rows(n, U, P, seed=12, zipf_s=1.1)
+    acct = pdp.NaiveBudgetAccountant(total_epsilon=1e6, total_delta=1e-6)
+    backend = pdp.HipBackend(sampling_seed=4, noise_seed=5)
+    engine = pdp.DPEngine(acct, backend)
+    params = pdp.AggregateParams(metrics=[pdp.Metrics.COUNT, pdp.Metrics.MEAN], max_partitions_contributed=3,
+                                 max_contributions_per_partition=2, min_value=0, max_value=10)
+    data = pdp.ColumnarData(partition=torch.from_numpy(pk).cuda(), privacy_id=torch.from_numpy(pid).cuda(),
+                            value=torch.from_numpy(val).cuda(), num_partitions=P, num_privacy_ids=U)
+    res = engine.aggregate(data, params, None)
+    sel = engine.select_partitions(data, pdp.SelectPartitionsParams(max_partitions_contributed=3), None)
+    acct.compute_budgets()
+    out = dict(res)
+    ref = o.bound_and_accumulate(pid, pk, val, P, o.BoundParams(3, 2, 0.0, 10.0), "feistel", seed=4)
+    for k, t in out.items():
+        assert abs(t.count - ref.count[k]) < 1e-2  # eps = 1e6 / 3 mechanisms: tiny noise
+    assert len(out) == int((ref.row_count > 0).sum())
+    kept = list(sel)
+    assert set(kept) == set(np.flatnonzero(ref.row_count > 0).tolist())
+
+
+# ---------------------------------------------------------------------------
+# Distributional tests (reference recipe: tests/dp_computations_test.py:69-129)
+# ---------------------------------------------------------------------------
+
+
+def _mass_checks(samples, sigma, within1, one_to_two):
+    n = len(samples)
+    a = np.abs(samples)
+    f1 = np.mean(a <= sigma)
+    f2 = np.mean((a > sigma) & (a <= 2 * sigma))
+    assert abs(f1 - within1) <= 2.4 * math.sqrt(within1 * (1 - within1) / n)
+    assert abs(f2 - one_to_two) <= 2.4 * math.sqrt(one_to_two * (1 - one_to_two) / n)
+
+
+@pytest.mark.parametrize("kind", ["laplace", "gaussian"])
+def test_noise_distribution(ex, kind):
+    """Noise on a zero count over 2e5 partitions: KS p >= 0.001 against numpy
+    and the 1-sigma / 1-2-sigma mass bands of the reference tests."""
+    import torch
+    from scipy import stats
+    from pipelinedp_amd.executor import Accumulators, BoundConfig, ReleaseConfig
+    P = 200000
+    acc = Accumulators(torch, P, ex.device, 1)
+    acc.row_count.zero_()
+    acc.count.zero_()
+    eps, delta, L0, Linf = 0.8, 1e-6, 3, 2
+    rel = ReleaseConfig(1, 0 if kind == "laplace" else 1, 0, [eps, 0, 0, 0, 0, 0], [delta, 0, 0, 0, 0, 0], 1, True,
+                        noise_seed=1234)
+    keep, out, fields = ex.release(acc, rel, BoundConfig(1, L0, Linf))
+    s = out[0].cpu().numpy()
+    rng = np.random.default_rng(0)
+    if kind == "laplace":
+        b = L0 * Linf / eps
+        ref = rng.laplace(0, b, P)
+        _mass_checks(s, math.sqrt(2) * b, 1 - math.exp(-math.sqrt(2)),
+                     math.exp(-math.sqrt(2)) - math.exp(-2 * math.sqrt(2)))
+    else:
+        sigma = o.gaussian_sigma(eps, delta, math.sqrt(L0) * Linf)
+        ref = rng.normal(0, sigma, P)
+        _mass_checks(s, sigma, 0.68268949213, 0.27181024396)
+    assert stats.ks_2samp(s, ref).pvalue >= 0.001
+
+
+def test_truncated_geometric_selection_rate(ex):
+    """Keep rate of partitions with n privacy ids ~ Binomial(p(n))."""
+    import torch
+    from pipelinedp_amd.executor import Accumulators, BoundConfig, ReleaseConfig
+    P = 100000
+    eps, delta, L0 = 1.0, 1e-2, 2
+    table = o.truncated_geometric_table(eps, delta, L0)
+    acc = Accumulators(torch, P, ex.device, 1)
+    nvals = np.arange(P) % 8 + 1
+    acc.row_count.copy_(torch.from_numpy(nvals))
+    acc.count.zero_()
+    rel = ReleaseConfig(1, 0, 1, [1.0, 0, 0, 0, 0, eps], [0, 0, 0, 0, 0, delta], 1, True, noise_seed=77)
+    keep, _, _ = ex.release(acc, rel, BoundConfig(1, L0, 1))
+    k = keep.cpu().numpy().astype(bool)
+    for nv in range(1, 9):
+        sel = nvals == nv
+        p = table[nv] if nv < len(table) else 1.0
+        m = sel.sum()
+        assert abs(k[sel].mean() - p) <= 4 * math.sqrt(p * (1 - p) / m) + 1e-12, (nv, k[sel].mean(), p)

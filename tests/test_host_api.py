@@ -1,0 +1,164 @@
+"""Host-side API parity with the reference (no GPU needed: aggregate() is lazy,
+so validation, budget requests and the explain report are all host work)."""
+import numpy as np
+import pytest
+
+import pipelinedp_amd as pdp
+from golden_util import aggregate_cases, load
+
+M = pdp.Metrics
+
+
+def test_budget_split_known_answer():
+    # tests/budget_accounting_test.py:56-70
+    acct = pdp.NaiveBudgetAccountant(total_epsilon=1, total_delta=1e-6)
+    b1 = acct.request_budget(mechanism_type=pdp.MechanismType.LAPLACE)
+    b2 = acct.request_budget(mechanism_type=pdp.MechanismType.GAUSSIAN, weight=3)
+    with pytest.raises(AssertionError):
+        _ = b1.eps
+    acct.compute_budgets()
+    assert (b1.eps, b1.delta, b2.eps, b2.delta) == (0.25, 0, 0.75, 1e-6)
+
+
+def test_budget_scopes_known_answer():
+    # tests/budget_accounting_test.py:72-110
+    acct = pdp.NaiveBudgetAccountant(total_epsilon=1, total_delta=1e-6)
+    with acct.scope(weight=0.4):
+        b1 = acct.request_budget(mechanism_type=pdp.MechanismType.LAPLACE)
+        b2 = acct.request_budget(mechanism_type=pdp.MechanismType.LAPLACE, weight=3)
+    with acct.scope(weight=0.6):
+        b3 = acct.request_budget(mechanism_type=pdp.MechanismType.LAPLACE)
+        b4 = acct.request_budget(mechanism_type=pdp.MechanismType.LAPLACE, weight=4)
+    acct.compute_budgets()
+    assert b1.eps == 0.4 * (1 / 4) and b2.eps == 0.4 * (3 / 4)
+    assert b3.eps == 0.6 * (1 / 5) and b4.eps == 0.6 * (4 / 5)
+    acct2 = pdp.NaiveBudgetAccountant(total_epsilon=1, total_delta=1e-6)
+    c1 = acct2.request_budget(mechanism_type=pdp.MechanismType.LAPLACE)
+    with acct2.scope(weight=0.5):
+        c2 = acct2.request_budget(mechanism_type=pdp.MechanismType.LAPLACE)
+    acct2.compute_budgets()
+    assert c1.eps == 1.0 / 1.5 and c2.eps == 0.5 / 1.5
+
+
+def test_budget_accountant_errors():
+    with pytest.raises(ValueError):
+        pdp.NaiveBudgetAccountant(total_epsilon=0, total_delta=1e-6)
+    with pytest.raises(ValueError):
+        pdp.NaiveBudgetAccountant(total_epsilon=1, total_delta=1)
+    acct = pdp.NaiveBudgetAccountant(total_epsilon=1, total_delta=0)
+    with pytest.raises(ValueError):
+        acct.request_budget(pdp.MechanismType.GAUSSIAN)
+    acct = pdp.NaiveBudgetAccountant(total_epsilon=1, total_delta=1e-6, num_aggregations=2)
+    acct._compute_budget_for_aggregation(1)
+    with pytest.raises(ValueError):
+        acct.compute_budgets()
+
+
+@pytest.mark.parametrize("kwargs,err", [
+    (dict(metrics=[M.SUM], max_partitions_contributed=1, max_contributions_per_partition=1), ValueError),
+    (dict(metrics=[M.COUNT], max_partitions_contributed=1), ValueError),
+    (dict(metrics=[M.COUNT], max_partitions_contributed=0, max_contributions_per_partition=1), ValueError),
+    (dict(metrics=[M.COUNT], max_partitions_contributed=1, max_contributions_per_partition=1, min_value=1),
+     ValueError),
+    (dict(metrics=[M.MEAN], max_partitions_contributed=1, max_contributions_per_partition=1, min_value=2,
+          max_value=1), ValueError),
+    (dict(metrics=[M.MEAN], max_partitions_contributed=1, max_contributions_per_partition=1,
+          min_sum_per_partition=0, max_sum_per_partition=1), ValueError),
+    (dict(metrics=[M.COUNT], max_partitions_contributed=1, max_contributions_per_partition=1, low=1), ValueError),
+    (dict(metrics=[M.PRIVACY_ID_COUNT], max_partitions_contributed=1, max_contributions_per_partition=1,
+          contribution_bounds_already_enforced=True), ValueError),
+    (dict(metrics=[M.SUM], max_partitions_contributed=1, max_contributions_per_partition=1, min_value=0,
+          max_value=float("inf")), ValueError),
+])
+def test_aggregate_params_validation(kwargs, err):
+    with pytest.raises(err):
+        pdp.AggregateParams(**kwargs)
+
+
+def test_engine_validation_errors():
+    acct = pdp.NaiveBudgetAccountant(1, 1e-6)
+    engine = pdp.DPEngine(acct, pdp.HipBackend())
+    params = pdp.AggregateParams(metrics=[M.COUNT], max_partitions_contributed=1, max_contributions_per_partition=1)
+    ex = pdp.DataExtractors(lambda r: r, lambda r: r, lambda r: r)
+    with pytest.raises(ValueError, match="col must be non-empty"):
+        engine.aggregate([], params, ex)
+    with pytest.raises(TypeError):
+        engine.aggregate([1], object(), ex)
+    with pytest.raises(ValueError, match="data_extractors"):
+        engine.aggregate([1], params, None)
+    p2 = pdp.AggregateParams(metrics=[M.COUNT], max_contributions=3)
+    with pytest.raises(NotImplementedError):
+        engine.aggregate([1], p2, ex)
+    p3 = pdp.AggregateParams(metrics=[M.PERCENTILE(50)], max_partitions_contributed=1,
+                             max_contributions_per_partition=1, min_value=0, max_value=1)
+    with pytest.raises(NotImplementedError):
+        engine.aggregate([1], p3, ex)
+    p4 = pdp.AggregateParams(metrics=[M.COUNT], max_partitions_contributed=1, max_contributions_per_partition=1,
+                             contribution_bounds_already_enforced=True)
+    with pytest.raises(ValueError, match="privacy_id_extractor"):
+        engine.aggregate([1], p4, ex)
+
+
+def test_result_is_lazy_and_needs_budgets():
+    acct = pdp.NaiveBudgetAccountant(1, 1e-6)
+    engine = pdp.DPEngine(acct, pdp.HipBackend())
+    params = pdp.AggregateParams(metrics=[M.COUNT], max_partitions_contributed=1, max_contributions_per_partition=1)
+
+    def exploding():
+        raise AssertionError("input must not be read at graph construction")
+        yield  # pragma: no cover
+
+    res = engine.aggregate(exploding(), params, pdp.DataExtractors(lambda r: r, lambda r: r, lambda r: r))
+    assert isinstance(res, pdp.DPResult)
+    with pytest.raises(AssertionError, match="not calculated yet"):
+        res._release_config(1)
+
+
+def _params_from_cfg(cfg):
+    metric = {"count": M.COUNT, "sum": M.SUM, "mean": M.MEAN, "variance": M.VARIANCE,
+              "privacy_id_count": M.PRIVACY_ID_COUNT}
+    kw = dict(metrics=[metric[m] for m in cfg["metrics"]], noise_kind=pdp.NoiseKind(cfg.get("noise_kind", "laplace")),
+              max_partitions_contributed=cfg["L0"], max_contributions_per_partition=cfg["Linf"],
+              contribution_bounds_already_enforced=cfg.get("already_enforced", False))
+    for k in ("min_value", "max_value", "min_sum_per_partition", "max_sum_per_partition"):
+        if cfg.get(k) is not None:
+            kw[k] = cfg[k]
+    return pdp.AggregateParams(**kw)
+
+
+@pytest.mark.parametrize("name", aggregate_cases())
+def test_explain_report_matches_reference(name):
+    """The explain-computation report (stages, budgets, parameter block) is
+    byte-identical to the one the reference produced for the golden case."""
+    d = load(name)
+    cfg = d["meta"]["cfg"]
+    acct = pdp.NaiveBudgetAccountant(total_epsilon=cfg.get("eps", 1.0), total_delta=cfg.get("delta", 1e-6))
+    engine = pdp.DPEngine(acct, pdp.HipBackend())
+    enforced = cfg.get("already_enforced", False)
+    ex = pdp.DataExtractors(privacy_id_extractor=None if enforced else (lambda r: r[0]),
+                            partition_extractor=lambda r: r[1], value_extractor=lambda r: r[2])
+    public = d["public"].tolist() if bool(d["has_public"]) else None
+    report = pdp.ExplainComputationReport()
+    engine.aggregate([(0, 0, 0.0)], _params_from_cfg(cfg), ex, public, out_explain_computaton_report=report)
+    acct.compute_budgets()
+    assert report.text() == d["meta"]["report"]
+
+
+def test_params_readable_string():
+    p = pdp.AggregateParams(metrics=[M.SUM], max_partitions_contributed=2, max_contributions_per_partition=10,
+                            min_value=1, max_value=5)
+    assert str(p) == ("AggregateParams:\n metrics=['SUM']\n noise_kind=laplace\n budget_weight=1\n"
+                      " Contribution bounding:\n  max_partitions_contributed=2\n"
+                      "  max_contributions_per_partition=10\n  min_value=1\n  max_value=5")
+
+
+def test_host_encoding():
+    from pipelinedp_amd.columnar import encode_rows
+    rows = [("u1", "a", 1.0), ("u2", "b", 2.0), ("u1", "c", 3.0), ("u3", "a", 4.0)]
+    ex = pdp.DataExtractors(lambda r: r[0], lambda r: r[1], lambda r: r[2])
+    e = encode_rows(rows, ex)
+    assert e.partition_keys == ["a", "b", "c"] and e.pk.tolist() == [0, 1, 2, 0]
+    assert e.pid.tolist() == [0, 1, 0, 2] and e.num_privacy_ids == 3
+    e = encode_rows(rows, ex, public_partitions=["c", "zz", "a", "c"])
+    assert e.partition_keys == ["c", "zz", "a"] and e.pk.tolist() == [2, -1, 0, 2]
+    np.testing.assert_array_equal(e.value, [1, 2, 3, 4])
