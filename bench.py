@@ -37,6 +37,7 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-profile", action="store_true")
     p.add_argument("--seed", type=int, default=20250204)
+    p.add_argument("--debug-flags", type=int, default=0, help="kernel ablation flags (experiments only)")
     return p.parse_args()
 
 
@@ -93,7 +94,8 @@ def main():
     ex = HipExecutor(local)
     pid, pk, val = ex.generate(n, U, P, seed=args.seed, zipf_s=args.zipf, lo=0.0, hi=10.0, row_offset=rank * n)
     mask = native.METRIC_COUNT | native.METRIC_SUM | native.METRIC_MEAN
-    bounds = BoundConfig(mask, args.l0, args.linf, 0.0, 10.0, sampling_seed=args.seed + 1)
+    bounds = BoundConfig(mask, args.l0, args.linf, 0.0, 10.0, sampling_seed=args.seed + 1,
+                         debug_flags=args.debug_flags)
     # NaiveBudgetAccountant(eps=1, delta=1e-6): MeanCombiner (Laplace) eps 0.5, selection eps 0.5 delta 1e-6
     eps = [0.0] * 6
     delta = [0.0] * 6

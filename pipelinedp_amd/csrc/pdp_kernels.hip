@@ -36,10 +36,6 @@ constexpr int kTile = kThreads * kItems;     // 4096 rows per radix tile
 constexpr int kMaxPasses = 8;
 constexpr int kHist = 257;                   // 256 digits + drop bucket
 constexpr int kStatusStride = 256;
-constexpr int kSegCap = 2048;                // rows per LDS batch
-constexpr int kSegItems = kSegCap / kThreads;
-constexpr int kIdxBits = 11;                 // log2(kSegCap)
-constexpr int kBucketTarget = 768;           // expected rows per pid bucket
 constexpr unsigned kOverflowCap = 1u << 16;
 constexpr unsigned kNumCounters = 64;
 
@@ -87,6 +83,7 @@ struct SegParams {
   int has_value;
   double a, b, mid;
   double smin, smax;
+  int debug;  // experiment flags: 1 skip emit, 2 skip sort, 4 skip sampling
 };
 
 struct AccPtrs {
@@ -431,254 +428,7 @@ __device__ __forceinline__ void emit_group(const SegParams& sp, const AccPtrs& a
   if (sp.want_y) atomicAdd(&acc.y[pk], y);
 }
 
-struct BucketSmem {
-  uint64_t key[kSegCap];
-  double val[kSegCap];
-  double gx[kSegCap];
-  double gy[kSegCap];
-  uint32_t pk[kSegCap];
-  uint32_t gpk[kSegCap];
-  uint32_t gcnt[kSegCap];
-  uint16_t gpos[kSegCap + 1];
-  uint16_t pfirst[kSegCap];
-  uint8_t gkeep[kSegCap];
-  int64_t tmp64[4];
-  unsigned int tmp32[4];
-};
-
-__device__ __forceinline__ bool is_bucket_start(const Rec* __restrict__ recs, int64_t p, int64_t n, int low) {
-  if (p >= n) return true;
-  if (p == 0) return true;
-  return (recs[p].pid >> low) != (recs[p - 1].pid >> low);
-}
-
-// Process rows [bs, be) (whole buckets, be - bs <= kSegCap).
-__device__ void process_batch(const Rec* __restrict__ recs, int64_t bs, int64_t be, const SegParams& sp,
-                              const AccPtrs& acc, const OvList& ov, BucketSmem& sm) {
-  const int t = threadIdx.x;
-  const int m = (int)(be - bs);
-  const uint32_t pid_base = (recs[bs].pid >> sp.low) << sp.low;
-
-  uint32_t rel[kSegItems];
-  uint32_t pkv[kSegItems];
-  uint32_t maxrel = 0;
-#pragma unroll
-  for (int k = 0; k < kSegItems; ++k) {
-    const int i = t + k * kThreads;
-    rel[k] = 0;
-    pkv[k] = 0;
-    if (i < m) {
-      const Rec r = recs[bs + i];
-      rel[k] = r.pid - pid_base;
-      pkv[k] = r.pk;
-      sm.pk[i] = r.pk;
-      sm.val[i] = r.val;
-      maxrel = rel[k] > maxrel ? rel[k] : maxrel;
-    }
-  }
-  maxrel = block_max(maxrel, sm.tmp32);
-  const int abits = pdp::ceil_log2_u64((uint64_t)maxrel + 1ull);
-  if (abits + sp.pkb + kIdxBits > 64) {
-    if (t == 0) record_overflow(ov, bs, be);
-    __syncthreads();
-    return;
-  }
-  const int shift_p = sp.pkb + kIdxBits;
-  int m2 = 1;
-  while (m2 < m) m2 <<= 1;
-#pragma unroll
-  for (int k = 0; k < kSegItems; ++k) {
-    const int i = t + k * kThreads;
-    if (i < m) {
-      const uint32_t pid = pid_base + rel[k];
-      const uint32_t pi = pdp::perm_bits(pkv[k], sp.pkb, pdp::pk_perm_key(sp.seed, pid));
-      sm.key[i] = ((uint64_t)rel[k] << shift_p) | ((uint64_t)pi << kIdxBits) | (uint64_t)i;
-    } else if (i < m2) {
-      sm.key[i] = ~0ull;
-    }
-  }
-  __syncthreads();
-
-  // Bitonic sort of m2 keys.
-  for (int size = 2; size <= m2; size <<= 1) {
-    for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      for (int c = t; c < (m2 >> 1); c += kThreads) {
-        const int i = 2 * stride * (c / stride) + (c % stride);
-        const int j = i + stride;
-        const bool asc = (i & size) == 0;
-        const uint64_t a = sm.key[i], b = sm.key[j];
-        if ((a > b) == asc) {
-          sm.key[i] = b;
-          sm.key[j] = a;
-        }
-      }
-      __syncthreads();
-    }
-  }
-
-  // Group (pid,pk) and pid structure over the sorted positions.
-  const int q0 = t * kSegItems;
-  uint64_t keys[kSegItems];
-  uint32_t gst_mask = 0, pst_mask = 0;
-  uint32_t cg = 0, cp = 0;
-#pragma unroll
-  for (int k = 0; k < kSegItems; ++k) {
-    const int q = q0 + k;
-    keys[k] = q < m ? sm.key[q] : ~0ull;
-    if (q < m) {
-      const uint64_t prev = q > 0 ? sm.key[q - 1] : 0ull;
-      const bool g = (q == 0) || ((keys[k] >> kIdxBits) != (prev >> kIdxBits));
-      const bool p = (q == 0) || ((keys[k] >> shift_p) != (prev >> shift_p));
-      gst_mask |= (uint32_t)g << k;
-      pst_mask |= (uint32_t)p << k;
-      cg += g;
-      cp += p;
-    }
-  }
-  unsigned int gtot, ptot;
-  const unsigned int gex = block_excl_scan(cg, sm.tmp32, gtot);
-  const unsigned int pex = block_excl_scan(cp, sm.tmp32, ptot);
-  {
-    unsigned int g = gex, p = pex;
-#pragma unroll
-    for (int k = 0; k < kSegItems; ++k) {
-      const int q = q0 + k;
-      if (q < m) {
-        if ((gst_mask >> k) & 1u) {
-          sm.gpos[g] = (uint16_t)q;
-          sm.gcnt[g] = 0;
-          sm.gx[g] = 0.0;
-          sm.gy[g] = 0.0;
-          ++g;
-        }
-        if ((pst_mask >> k) & 1u) {
-          sm.pfirst[p] = (uint16_t)(g - 1);
-          ++p;
-        }
-      }
-    }
-  }
-  if (t == 0) sm.gpos[gtot] = (uint16_t)m;
-  __syncthreads();
-
-  // Rows: sampling decision + run-length accumulation per group.
-  {
-    int g = (int)gex - 1, p = (int)pex - 1;
-    int run_g = -1;
-    uint32_t run_c = 0;
-    double run_x = 0.0, run_y = 0.0;
-#pragma unroll
-    for (int k = 0; k < kSegItems; ++k) {
-      const int q = q0 + k;
-      if (q < m) {
-        if ((gst_mask >> k) & 1u) ++g;
-        if ((pst_mask >> k) & 1u) ++p;
-        const int gs = sm.gpos[g];
-        const int ng = (int)sm.gpos[g + 1] - gs;
-        const int j = q - gs;
-        const int grank = g - (int)sm.pfirst[p];
-        const int idx = (int)(keys[k] & ((1u << kIdxBits) - 1u));
-        const uint32_t pkr = sm.pk[idx];
-        const uint32_t pid = pid_base + (uint32_t)(keys[k] >> shift_p);
-        if (j == 0) {
-          sm.gpk[g] = pkr;
-          sm.gkeep[g] = (uint8_t)(grank < sp.l0);
-        }
-        bool kept = grank < sp.l0;
-        if (kept && ng > sp.linf)
-          kept = pdp::cycle_walk((uint32_t)j, (uint64_t)ng, pdp::group_perm_key(sp.seed, pid, pkr)) <
-                 (uint64_t)sp.linf;
-        if (kept) {
-          if (g != run_g) {
-            if (run_g >= 0) {
-              atomicAdd(&sm.gcnt[run_g], run_c);
-              if (sp.xmode != kXNone) atomicAdd(&sm.gx[run_g], run_x);
-              if (sp.want_y) atomicAdd(&sm.gy[run_g], run_y);
-            }
-            run_g = g;
-            run_c = 0;
-            run_x = 0.0;
-            run_y = 0.0;
-          }
-          double x, y;
-          row_terms(sp, sm.val[idx], x, y);
-          ++run_c;
-          run_x += x;
-          run_y += y;
-        }
-      }
-    }
-    if (run_g >= 0) {
-      atomicAdd(&sm.gcnt[run_g], run_c);
-      if (sp.xmode != kXNone) atomicAdd(&sm.gx[run_g], run_x);
-      if (sp.want_y) atomicAdd(&sm.gy[run_g], run_y);
-    }
-  }
-  __syncthreads();
-
-  for (int g = t; g < (int)gtot; g += kThreads) {
-    if (sm.gkeep[g] && sm.gcnt[g] > 0) emit_group(sp, acc, sm.gpk[g], sm.gcnt[g], sm.gx[g], sm.gy[g]);
-  }
-  __syncthreads();
-}
-
-__global__ __launch_bounds__(kThreads) void k_buckets(const Rec* __restrict__ recs,
-                                                      const unsigned long long* __restrict__ counters_n,
-                                                      int n_slot, SegParams sp, AccPtrs acc, OvList ov,
-                                                      int force_fallback) {
-  __shared__ BucketSmem sm;
-  const int t = threadIdx.x;
-  const int64_t n = (int64_t)counters_n[n_slot];
-  const int64_t lo = (int64_t)blockIdx.x * kSegCap;
-  if (lo >= n) return;
-  const int64_t hi = lo + kSegCap < n ? lo + kSegCap : n;
-  const int64_t kNone = INT64_MAX;
-
-  int64_t s = kNone;
-  for (int64_t p = lo + t; p < hi; p += kThreads)
-    if (is_bucket_start(recs, p, n, sp.low)) {
-      s = p;
-      break;
-    }
-  s = block_min(s, sm.tmp64);
-  if (s == kNone) return;
-
-  int64_t cur = s;
-  while (cur < hi) {
-    const int64_t wend = cur + kSegCap < n ? cur + kSegCap : n;
-    int64_t fgh = kNone;
-    for (int64_t p = cur + 1 + t; p <= wend; p += kThreads)
-      if (p >= hi && is_bucket_start(recs, p, n, sp.low)) {
-        fgh = p;
-        break;
-      }
-    fgh = block_min(fgh, sm.tmp64);
-    const int64_t limit = fgh < wend ? fgh : wend;
-    int64_t be = -1;
-    for (int64_t p = cur + 1 + t; p <= limit; p += kThreads)
-      if (is_bucket_start(recs, p, n, sp.low)) be = p;
-    be = block_max(be, sm.tmp64);
-    if (be < 0) {
-      // Bucket at cur is larger than one LDS batch: find its end.
-      int64_t bend = kNone;
-      for (int64_t chunk = wend + 1; bend == kNone; chunk += kThreads) {
-        int64_t c = kNone;
-        const int64_t p = chunk + t;
-        if (p <= n && is_bucket_start(recs, p, n, sp.low)) c = p;
-        bend = block_min(c, sm.tmp64);
-      }
-      if (t == 0) record_overflow(ov, cur, bend);
-      cur = bend;
-      continue;
-    }
-    if (force_fallback) {
-      if (t == 0) record_overflow(ov, cur, be);
-    } else {
-      process_batch(recs, cur, be, sp, acc, ov, sm);
-    }
-    cur = be;
-  }
-}
+#include "pdp_segments.inc"
 
 // ---------------------------------------------------------------------------
 // KF: generic sorted-stream path (fallback for buckets that overflow LDS)
@@ -1004,8 +754,8 @@ Plan make_plan(int64_t n, int64_t U, int64_t P) {
   p.pidb = std::max(1, pdp::ceil_log2_u64((uint64_t)U));
   p.pkb = std::max(1, pdp::ceil_log2_u64((uint64_t)P));
   const double rows_per_pid = (double)n / (double)U;
-  p.low = 0;
-  while (p.low < p.pidb && rows_per_pid * (double)(1ull << (p.low + 1)) <= kBucketTarget) ++p.low;
+  p.low = 0;  // full sort by pid: segments are contiguous (k_segments)
+  (void)rows_per_pid;
   const int kb = p.pidb - p.low;
   p.passes = std::max(1, (kb + 7) / 8);
   int rem = kb;
@@ -1040,6 +790,7 @@ SegParams make_seg(const pdp_bound_params* bp, int low, int pkb, bool has_value)
   sp.mid = bp->min_value + (bp->max_value - bp->min_value) / 2;  // dp_computations.py:65-69
   sp.smin = bp->min_sum_per_partition;
   sp.smax = bp->max_sum_per_partition;
+  sp.debug = bp->reserved;
   return sp;
 }
 
@@ -1405,7 +1156,7 @@ int pdp_bound_accumulate(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_
     return fail(PDP_ERR_INVALID_ARG, "contribution bounds must be positive");
   const int m = bp->metrics;
   const bool need_value = (m & (PDP_METRIC_SUM | PDP_METRIC_MEAN | PDP_METRIC_VARIANCE)) != 0;
-  if (need_value && !cols->value) return fail(PDP_ERR_INVALID_ARG, "value column required for SUM/MEAN/VARIANCE");
+  if (need_value && n > 0 && !cols->value) return fail(PDP_ERR_INVALID_ARG, "value column required for SUM/MEAN/VARIANCE");
   if (n > 0 && !cols->pk) return fail(PDP_ERR_INVALID_ARG, "pk column required");
   if (!bp->bounds_already_enforced && n > 0 && !cols->pid) return fail(PDP_ERR_INVALID_ARG, "pid column required");
   if (!accp->row_count) return fail(PDP_ERR_INVALID_ARG, "row_count accumulator required");
@@ -1498,10 +1249,10 @@ int pdp_bound_accumulate(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_
   Rec* spare = dst;
 
   OvList ov{ranges, counters};
-  const int64_t seg_grid = (n + kSegCap - 1) / kSegCap;
+  const int64_t seg_grid = (n + kSegTile - 1) / kSegTile;
   {
     ProfScope ps(ctx, PDP_STAGE_BUCKETS, stream);
-    hipLaunchKernelGGL(k_buckets, dim3((unsigned)seg_grid), dim3(kThreads), 0, stream, sorted, counters,
+    hipLaunchKernelGGL(k_segments, dim3((unsigned)seg_grid), dim3(kThreads), 0, stream, sorted, counters,
                        (int)kCtrNKept, sp, acc, ov, (int)bp->debug_force_fallback);
   }
   HIP_TRY(hipGetLastError());

@@ -25,6 +25,7 @@ class BoundConfig:
     bounds_already_enforced: bool = False
     sampling_seed: Optional[int] = None
     debug_force_fallback: bool = False
+    debug_flags: int = 0
 
 
 @dataclasses.dataclass
@@ -118,7 +119,7 @@ class HipExecutor:
             int(cfg.min_sum_per_partition is not None),
             float(cfg.min_value or 0.0), float(cfg.max_value or 0.0),
             float(cfg.min_sum_per_partition or 0.0), float(cfg.max_sum_per_partition or 0.0),
-            seed, int(cfg.debug_force_fallback), 0)
+            seed, int(cfg.debug_force_fallback), int(cfg.debug_flags))
         if acc is None:
             acc = Accumulators(torch, num_partitions, self.device, cfg.metrics_mask)
         nbytes = ctypes.c_size_t(0)

@@ -239,9 +239,12 @@ def test_engine_columnar_device_input_and_select_partitions():
     ref = o.bound_and_accumulate(pid, pk, val, P, o.BoundParams(3, 2, 0.0, 10.0), "feistel", seed=4)
     for k, t in out.items():
         assert abs(t.count - ref.count[k]) < 1e-2  # eps = 1e6 / 3 mechanisms: tiny noise
-    assert len(out) == int((ref.row_count > 0).sum())
-    kept = list(sel)
-    assert set(kept) == set(np.flatnonzero(ref.row_count > 0).tolist())
+    # huge eps: truncated geometric keeps every partition with >= 2 privacy
+    # ids, those with exactly one only with probability delta / L0.
+    many = set(np.flatnonzero(ref.row_count >= 2).tolist())
+    assert many <= set(out) <= set(np.flatnonzero(ref.row_count >= 1).tolist())
+    kept = set(sel)
+    assert many <= kept <= set(np.flatnonzero(ref.row_count >= 1).tolist())
 
 
 # ---------------------------------------------------------------------------
