@@ -62,7 +62,7 @@ def cpu_baseline(args, P):
     spec = o.ReleaseSpec(("mean", "count", "sum"), "laplace", {"mean": (0.5, 0.0)}, "truncated_geometric",
                          (0.5, 1e-6))
     t0 = time.perf_counter()
-    acc = o.bound_and_accumulate(pid, pk, val, P, bp, "feistel", seed=1)
+    acc = o.bound_and_accumulate(pid, pk, val, P, bp, "hash", seed=1)
     o.release(acc, bp, spec, seed=2)
     dt = time.perf_counter() - t0
     return {"value": m / dt, "unit": "rows/s", "cores": 1, "kind": "port",

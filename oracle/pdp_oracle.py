@@ -20,11 +20,12 @@ Each function cites the reference file:line it restates.
 
 Randomness specification (shared bit-for-bit with the HIP kernels, see
 DESIGN.md "Randomness"):
-  * sampling (contribution bounding) uses a keyed Feistel permutation
-    (``perm_bits``) and cycle walking (``cycle_walk``): the kept L_inf rows of a
-    (pid, pk) group are the rows whose input-order rank j satisfies
-    cw_perm(j) < L_inf; the kept L0 partitions of a pid are the L0 smallest
-    pi_pid(pk).  ``sampler='feistel'`` reproduces the GPU exactly;
+  * sampling (contribution bounding) ranks 64-bit splitmix priorities: the
+    kept L_inf rows of a (pid, pk) group are the L_inf rows with the smallest
+    (row_priority(j), j), j = input-order rank in the group; the kept L0
+    partitions of a pid are the L0 with the smallest (group_priority, pk).
+    This is exactly uniform sampling without replacement (given the hash).
+    ``sampler='hash'`` reproduces the GPU exactly;
     ``sampler='numpy'`` draws uniform subsets with numpy like LocalBackend
     (``pipeline_backend.py:504-520``).
   * noise / selection draws use Philox4x32-10 keyed by the 64-bit noise seed
@@ -68,28 +69,41 @@ def _mask(bits):
     return np.uint64((1 << int(bits)) - 1) if bits > 0 else np.uint64(0)
 
 
-_FEISTEL_ROUND_C = 0xD1B54A32D192ED03
+_M32 = np.uint64(0xFFFFFFFF)
+
+
+def fmix32(h):
+    """murmur3 32-bit finaliser on uint64 arrays holding 32-bit values."""
+    h = _u64(h) & _M32
+    h ^= h >> np.uint64(16)
+    h = (h * np.uint64(0x85EBCA6B)) & _M32
+    h ^= h >> np.uint64(13)
+    h = (h * np.uint64(0xC2B2AE35)) & _M32
+    h ^= h >> np.uint64(16)
+    return h
+
+
+def _mask32(bits):
+    return np.uint64((1 << int(bits)) - 1) if bits > 0 else np.uint64(0)
 
 
 def perm_bits(x, bits, key):
-    """Keyed 4-round Feistel bijection on [0, 2**bits) (bits <= 32).
-
-    ``bits`` is a python int (uniform over the array) and ``key`` a uint64
-    array broadcastable with ``x``.
-    """
+    """Keyed 4-round Feistel bijection on [0, 2**bits) (bits <= 32) with
+    round function F_r(R) = fmix32(R * 0x9E3779B1 + k_r), round keys
+    (lo32(key), hi32(key), lo32 ^ 0x85EBCA6B, hi32 ^ 0xC2B2AE35)."""
     x = _u64(x)
     key = _u64(key)
+    k0, k1 = key & _M32, key >> np.uint64(32)
+    rk = [k0, k1, k0 ^ np.uint64(0x85EBCA6B), k1 ^ np.uint64(0xC2B2AE35)]
     h1 = (bits + 1) >> 1
     h2 = bits >> 1
     wl, wr = h1, h2
     left = x >> np.uint64(h2)
-    right = x & _mask(h2)
+    right = x & _mask32(h2)
     with np.errstate(over="ignore"):
         for r in range(4):
-            f = splitmix64(key + np.uint64((_FEISTEL_ROUND_C * (r + 1)) & 0xFFFFFFFFFFFFFFFF) + right)
-            new_left = right
-            new_right = left ^ (f & _mask(wl))
-            left, right = new_left, new_right
+            f = fmix32((right * np.uint64(0x9E3779B1) + rk[r]) & _M32)
+            left, right = right, left ^ (f & _mask32(wl))
             wl, wr = wr, wl
     return (left << np.uint64(h2)) | right
 
@@ -129,23 +143,29 @@ def cycle_walk(j, n, key):
     return out
 
 
-def pk_perm_key(seed, pid):
-    """Key of pi_pid (partition order used for L0 sampling)."""
+def pid_key(seed, pid):
+    """Per privacy-id key: splitmix64(seed ^ splitmix64(pid + 1))."""
     with np.errstate(over="ignore"):
         return splitmix64(_u64(seed) ^ splitmix64(_u64(pid) + np.uint64(1)))
 
 
-def group_perm_key(seed, pid, pk):
-    """Key of the per-(pid, pk) permutation used for L_inf sampling."""
+def group_priority(seed, pid, pk):
+    """L0 priority of partition pk for privacy id pid."""
     with np.errstate(over="ignore"):
-        return splitmix64(pk_perm_key(seed, pid) ^ splitmix64(_u64(pk) + np.uint64(0x632BE59BD9B4E019)))
+        return splitmix64(pid_key(seed, pid) + (_u64(pk) + np.uint64(1)) * np.uint64(0xD1B54A32D192ED03))
+
+
+def row_priority(gprio, j):
+    """L_inf priority of the j-th (input order) row of a (pid, pk) group."""
+    with np.errstate(over="ignore"):
+        gkey = splitmix64(_u64(gprio) ^ np.uint64(0xA0761D6478BD642F))
+        return splitmix64(gkey + (_u64(j) + np.uint64(1)) * np.uint64(0x9E3779B97F4A7C15))
 
 
 _PHILOX_M0 = np.uint64(0xD2511F53)
 _PHILOX_M1 = np.uint64(0xCD9E8D57)
 _PHILOX_W0 = np.uint64(0x9E3779B9)
 _PHILOX_W1 = np.uint64(0xBB67AE85)
-_M32 = np.uint64(0xFFFFFFFF)
 
 
 def philox4x32_10(c0, c1, c2, c3, k0, k1):
@@ -370,14 +390,14 @@ def _group_starts(keys_sorted_list):
 
 
 def bound_and_accumulate(pid, pk, value, num_partitions, params: BoundParams,
-                         sampler="feistel", seed=0, rng=None) -> Accumulators:
+                         sampler="hash", seed=0, rng=None) -> Accumulators:
     """SamplingCrossAndPerPartitionContributionBounder.bound_contributions
     (contribution_bounders.py:66-105) + CompoundCombiner.create_accumulator /
     merge_accumulators (combiners.py:558-573) + combine_accumulators_per_key
     (pipeline_backend.py:528-538), dense over partitions [0, num_partitions).
 
     Rows with pk < 0 are dropped (non-public partitions,
-    dp_engine.py:283-293).  ``sampler``: 'feistel' (GPU-identical),
+    dp_engine.py:283-293).  ``sampler``: 'hash' (GPU-identical),
     'numpy' (uniform subsets from ``rng``, like LocalBackend), or 'none'
     (keep everything; valid when bounds are non-binding).
     """
@@ -430,13 +450,18 @@ def bound_and_accumulate(pid, pk, value, num_partitions, params: BoundParams,
     j = np.arange(n) - gfirst[gid]
     gn = gsize[gid]
 
+    if sampler == "hash":
+        sampler = "hash"
+    g_pid = spid[gfirst]
+    g_pk = spk[gfirst]
     # --- per-partition (L_inf) sampling, contribution_bounders.py:74-76
-    if sampler == "feistel":
-        big = gn > Linf
-        keep = np.ones(n, dtype=bool)
-        if big.any():
-            key = group_perm_key(seed, spid[big], spk[big])
-            keep[big] = cycle_walk(j[big], gn[big], key) < np.uint64(Linf)
+    if sampler == "hash":
+        gprio = group_priority(seed, g_pid, g_pk)
+        rprio = row_priority(gprio[gid], j)
+        o2 = np.lexsort((j, rprio, gid))
+        rank = np.empty(n, dtype=np.int64)
+        rank[o2] = np.arange(n) - gfirst[gid[o2]]
+        keep = rank < Linf
     elif sampler == "numpy":
         rng = rng or np.random.default_rng()
         prio = rng.random(n)
@@ -470,12 +495,8 @@ def bound_and_accumulate(pid, pk, value, num_partitions, params: BoundParams,
                             params.max_sum_per_partition)
 
     # --- cross-partition (L0) sampling, contribution_bounders.py:87-92
-    g_pid = spid[gfirst]
-    g_pk = spk[gfirst]
-    if sampler == "feistel":
-        pkb = max(1, ceil_log2(P))
-        pi = perm_bits(_u64(g_pk), pkb, pk_perm_key(seed, g_pid))
-        o3 = np.lexsort((pi, g_pid))
+    if sampler == "hash":
+        o3 = np.lexsort((g_pk, gprio, g_pid))
     elif sampler == "numpy":
         o3 = np.lexsort((rng.random(G), g_pid))
     else:

@@ -4,16 +4,16 @@
 // Pipeline of pdp_bound_accumulate (main path):
 //   K0 k_histogram  : one read of pid/pk -> digit histograms of every radix
 //                     pass (+ count of dropped / invalid rows)
-//   K1 k_onesweep   : LSD radix passes on key = pid >> low (stable, decoupled
+//   K1 k_onesweep   : stable LSD radix passes on the privacy id (decoupled
 //                     look-back); pass 0 packs the SoA int64/int64/f64 columns
 //                     into 16-byte records and drops non-public rows
-//   K2 k_buckets    : per workgroup, LDS batches of whole privacy-id buckets:
-//                     bitonic sort by (pid, pi_pid(pk), input order), L_inf and
-//                     L0 uniform sampling, clipping, per-(pid,pk) accumulators,
-//                     fp64/int64 atomics into the dense [P] partition
-//                     accumulators.  Buckets that do not fit LDS go to:
-//   KF generic path : LSD sort by (pid, pi_pid(pk)) + device-wide scans
-//                     (rare; exact same semantics).
+//   K2 k_segments   : per privacy-id segment batches, one wave each: register
+//                     bitonic sort by (pid, pk, row), L0 / L_inf sampling by
+//                     ranked hash priorities, clipping, per-(pid,pk) sums,
+//                     fp64/int64 atomics into the dense [P] accumulators
+//                     (k_segments_big for 257..1024-row batches)
+//   KF generic path : segments > 1024 rows: LSD sorts + device-wide scans
+//                     (rare; exactly the same sampling).
 // pdp_release: K5/K6 k_release — selection + Laplace/Gaussian noise from
 // Philox, one thread per partition.
 #include <hip/hip_runtime.h>
@@ -33,7 +33,7 @@ namespace {
 constexpr int kThreads = 256;
 constexpr int kItems = 16;                   // rows per thread in a radix tile
 constexpr int kTile = kThreads * kItems;     // 4096 rows per radix tile
-constexpr int kMaxPasses = 8;
+constexpr int kMaxPasses = 12;
 constexpr int kHist = 257;                   // 256 digits + drop bucket
 constexpr int kStatusStride = 256;
 constexpr unsigned kOverflowCap = 1u << 16;
@@ -46,6 +46,8 @@ enum Counter {
   kCtrFull = 3,
   kCtrErr = 4,
   kCtrNGeneric = 5,
+  kCtrNBig = 6,
+  kCtrBigNext = 7,
   kCtrTile0 = 16,  // 16..63 tile claim counters, one per onesweep launch
 };
 
@@ -56,7 +58,7 @@ struct __align__(16) Rec {
 };
 
 struct KeySpec {
-  int mode;  // 0: key = pid >> low ; 1: key = (pid << pkb) | pi_pid(pk)
+  int mode;  // 0: key = pid >> low ; 1: key = (pid << pkb) | pk ; 3: key = (pid, bits(val)) 96-bit
   int passes;
   int shift[kMaxPasses];
   int bits[kMaxPasses];
@@ -98,14 +100,21 @@ struct OvList {
   unsigned long long* counters;
 };
 
-__device__ __forceinline__ uint64_t sort_key(const KeySpec& ks, uint32_t pid, uint32_t pk) {
-  if (ks.mode == 0) return (uint64_t)(pid >> ks.low);
-  const uint32_t pi = pdp::perm_bits(pk, ks.pkb, pdp::pk_perm_key(ks.seed, pid));
-  return ((uint64_t)pid << ks.pkb) | pi;
-}
-
-__device__ __forceinline__ uint32_t digit_of(const KeySpec& ks, int pass, uint64_t key) {
-  return (uint32_t)((key >> ks.shift[pass]) & ((1ull << ks.bits[pass]) - 1ull));
+// Digit of radix pass `pass` of record r.  Mode 3 sorts by the 96-bit key
+// (pid field, bit pattern of val): passes with shift >= 64 read the pid field.
+__device__ __forceinline__ uint32_t digit_of(const KeySpec& ks, int pass, const Rec& r) {
+  const uint64_t mask = (1ull << ks.bits[pass]) - 1ull;
+  const int sh = ks.shift[pass];
+  uint64_t key;
+  if (ks.mode == 0) {
+    key = (uint64_t)(r.pid >> ks.low);
+  } else if (ks.mode == 1) {
+    key = ((uint64_t)r.pid << ks.pkb) | (uint64_t)r.pk;
+  } else {
+    if (sh >= 64) return (uint32_t)(((uint64_t)r.pid >> (sh - 64)) & mask);
+    key = (uint64_t)__double_as_longlong(r.val);
+  }
+  return (uint32_t)((key >> sh) & mask);
 }
 
 __device__ __forceinline__ double clip(double v, double lo, double hi) {
@@ -197,7 +206,7 @@ __global__ __launch_bounds__(kThreads) void k_histogram(const int64_t* __restric
   unsigned int invalid = 0;
   const int64_t stride = (int64_t)gridDim.x * kThreads;
   for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < n; i += stride) {
-    uint32_t p32, k32;
+    Rec r;
     if (SOA) {
       const int64_t a = pid[i], b = pk[i];
       if (b < 0 || b >= (int64_t)ks.num_parts || a < 0 || a >= (int64_t)ks.num_pids) {
@@ -205,15 +214,13 @@ __global__ __launch_bounds__(kThreads) void k_histogram(const int64_t* __restric
         atomicAdd(&sh[256], 1u);
         continue;
       }
-      p32 = (uint32_t)a;
-      k32 = (uint32_t)b;
+      r.pid = (uint32_t)a;
+      r.pk = (uint32_t)b;
+      r.val = 0.0;
     } else {
-      const Rec r = rin[i];
-      p32 = r.pid;
-      k32 = r.pk;
+      r = rin[i];
     }
-    const uint64_t key = sort_key(ks, p32, k32);
-    for (int p = 0; p < ks.passes; ++p) atomicAdd(&sh[p * kHist + digit_of(ks, p, key)], 1u);
+    for (int p = 0; p < ks.passes; ++p) atomicAdd(&sh[p * kHist + digit_of(ks, p, r)], 1u);
   }
   __syncthreads();
   for (int i = threadIdx.x; i < ks.passes * kHist; i += kThreads)
@@ -290,10 +297,10 @@ __global__ __launch_bounds__(kThreads, 2) void k_onesweep(
         if (b < 0 || b >= (int64_t)ks.num_parts || a < 0 || a >= (int64_t)ks.num_pids)
           d = 256;  // dropped
         else
-          d = digit_of(ks, pass, sort_key(ks, r[k].pid, r[k].pk));
+          d = digit_of(ks, pass, r[k]);
       } else {
         r[k] = rin[idx];
-        d = digit_of(ks, pass, sort_key(ks, r[k].pid, r[k].pk));
+        d = digit_of(ks, pass, r[k]);
       }
     }
     dg[k] = d;
@@ -505,42 +512,65 @@ __global__ void k_stream_starts(const long long* __restrict__ gs_raw_scan, const
   }
 }
 
+// L_inf priorities: R2[i] = {group id, row index, bits(row priority)}.
+__global__ void k_stream_row_prio(const Rec* __restrict__ r, int64_t m, const long long* __restrict__ gsc,
+                                  const long long* __restrict__ gpos, uint64_t seed, Rec* __restrict__ out) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (int64_t)gridDim.x * blockDim.x) {
+    const long long g = gsc[i] - 1;
+    const Rec a = r[i];
+    const uint64_t gp = pdp::group_priority(pdp::pid_key(seed, a.pid), a.pk);
+    const uint64_t rp = pdp::row_priority(gp, (uint64_t)(i - gpos[g]));
+    out[i] = Rec{(uint32_t)g, (uint32_t)i, __longlong_as_double((long long)rp)};
+  }
+}
+
+// L0 priorities: R3[g] = {pid ordinal, group id, bits(group priority)}.
+__global__ void k_stream_group_prio(const Rec* __restrict__ r, const long long* __restrict__ psc,
+                                    const long long* __restrict__ gpos, int64_t ngroups, uint64_t seed,
+                                    Rec* __restrict__ out) {
+  for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < ngroups;
+       g += (int64_t)gridDim.x * blockDim.x) {
+    const long long q = gpos[g];
+    const Rec a = r[q];
+    const uint64_t gp = pdp::group_priority(pdp::pid_key(seed, a.pid), a.pk);
+    out[g] = Rec{(uint32_t)(psc[q] - 1), (uint32_t)g, __longlong_as_double((long long)gp)};
+  }
+}
+
+// Sorted (group, priority) records -> rank within the group segment.
+__global__ void k_stream_ranks(const Rec* __restrict__ sorted, int64_t m, const long long* __restrict__ seg_first,
+                               int64_t limit, uint8_t* __restrict__ keep8, int32_t* __restrict__ rank32) {
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < m; q += (int64_t)gridDim.x * blockDim.x) {
+    const Rec a = sorted[q];
+    const long long rank = q - seg_first[a.pid];
+    if (keep8) keep8[a.pk] = rank < limit;
+    if (rank32) rank32[a.pk] = (int32_t)(rank < 0x7FFFFFFF ? rank : 0x7FFFFFFF);
+  }
+}
+
 __global__ void k_stream_rows(const Rec* __restrict__ r, int64_t m, const long long* __restrict__ gsc,
-                              const long long* __restrict__ psc, const long long* __restrict__ gpos,
-                              const long long* __restrict__ pfirst, SegParams sp,
+                              const int32_t* __restrict__ grank, const uint8_t* __restrict__ row_keep, SegParams sp,
                               unsigned long long* __restrict__ gcnt, double* __restrict__ gx,
                               double* __restrict__ gy) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (int64_t)gridDim.x * blockDim.x) {
-    const long long g = gsc[i] - 1, p = psc[i] - 1;
-    const long long grank = g - pfirst[p];
-    if (grank >= sp.l0) continue;
-    const long long gs0 = gpos[g];
-    const long long ng = gpos[g + 1] - gs0;
-    const long long j = i - gs0;
-    const Rec a = r[i];
-    bool kept = true;
-    if (ng > sp.linf)
-      kept = pdp::cycle_walk((uint32_t)j, (uint64_t)ng, pdp::group_perm_key(sp.seed, a.pid, a.pk)) <
-             (uint64_t)sp.linf;
-    if (!kept) continue;
+    const long long g = gsc[i] - 1;
+    if (grank[g] >= sp.l0 || !row_keep[i]) continue;
     double x, y;
-    row_terms(sp, a.val, x, y);
+    row_terms(sp, r[i].val, x, y);
     atomicAdd(&gcnt[g], 1ull);
     if (sp.xmode != kXNone) atomicAdd(&gx[g], x);
     if (sp.want_y) atomicAdd(&gy[g], y);
   }
 }
 
-__global__ void k_stream_groups(const Rec* __restrict__ r, const long long* __restrict__ psc,
-                                const long long* __restrict__ gpos, const long long* __restrict__ pfirst,
-                                int64_t ngroups, SegParams sp, const unsigned long long* __restrict__ gcnt,
-                                const double* __restrict__ gx, const double* __restrict__ gy, AccPtrs acc) {
+__global__ void k_stream_groups(const Rec* __restrict__ r, const long long* __restrict__ gpos,
+                                const int32_t* __restrict__ grank, int64_t ngroups, SegParams sp,
+                                const unsigned long long* __restrict__ gcnt, const double* __restrict__ gx,
+                                const double* __restrict__ gy, AccPtrs acc) {
   for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < ngroups;
        g += (int64_t)gridDim.x * blockDim.x) {
-    const long long q = gpos[g];
-    const long long p = psc[q] - 1;
-    if (g - pfirst[p] >= sp.l0 || gcnt[g] == 0) continue;
-    emit_group(sp, acc, r[q].pk, (uint32_t)gcnt[g], gx[g], gy[g]);
+    if (grank[g] >= sp.l0 || gcnt[g] == 0) continue;
+    emit_group(sp, acc, r[gpos[g]].pk, (uint32_t)gcnt[g], gx[g], gy[g]);
   }
 }
 
@@ -724,8 +754,9 @@ int grid_for(int64_t n, int threads, int cap = 4096) {
 }
 
 struct Layout {
-  size_t recs_a, recs_b, hist, off, counters, status, ranges, total;
+  size_t recs_a, recs_b, hist, off, counters, status, ranges, big, total;
   int64_t tiles;
+  uint64_t big_cap;
 };
 
 Layout layout_for(int64_t n) {
@@ -740,6 +771,8 @@ Layout layout_for(int64_t n) {
   L.tiles = (std::max<int64_t>(n, 1) + kTile - 1) / kTile;
   L.status = o; o += align_up((size_t)L.tiles * kStatusStride * 8, 256);
   L.ranges = o; o += align_up((size_t)kOverflowCap * 16, 256);
+  L.big_cap = (uint64_t)std::max<int64_t>(n, 1) / (kSmallMax + 1) + 64;
+  L.big = o; o += align_up((size_t)L.big_cap * 16, 256);
   L.total = o;
   return L;
 }
@@ -798,6 +831,7 @@ SegParams make_seg(const pdp_bound_params* bp, int low, int pkb, bool has_value)
 
 struct pdp_ctx {
   int device = 0;
+  unsigned int tile_slot = 16;  // next free onesweep tile-claim counter
   bool prof = false;
   struct ProfRec {
     int stage;
@@ -877,26 +911,19 @@ int scan_inplace(long long* a, int64_t n, hipStream_t stream) {
   return 0;
 }
 
-// Full LSD sort of `m` records in `a` by (pid, pi_pid(pk)); result pointer
-// returned via out (either a or b).
-int sort_pid_pk(pdp_ctx* ctx, Rec* a, Rec* b, int64_t m, const Plan& plan, uint64_t seed, uint32_t U, uint32_t P,
-                unsigned long long* hist, unsigned long long* off, unsigned long long* counters,
-                unsigned long long* status, size_t status_bytes, void* ws, int tile_slot0, hipStream_t stream,
-                Rec** out) {
-  KeySpec ks{};
-  ks.mode = 1;
-  ks.low = 0;
-  ks.pkb = plan.pkb;
-  ks.seed = seed;
-  ks.num_pids = U;
-  ks.num_parts = P;
-  const int kb = plan.pidb + plan.pkb;
-  ks.passes = (kb + 7) / 8;
-  int sh = 0;
-  for (int i = 0; i < ks.passes; ++i) {
-    ks.shift[i] = sh;
-    ks.bits[i] = std::min(8, kb - sh);
-    sh += ks.bits[i];
+// LSD sort of `m` records (a <-> b ping-pong) by the passes of `ks`; the
+// sorted array pointer is returned in *out.
+int sort_recs(pdp_ctx* ctx, Rec* a, Rec* b, int64_t m, const KeySpec& ks, unsigned long long* hist,
+              unsigned long long* off, unsigned long long* counters, unsigned long long* status, size_t status_bytes,
+              void* ws, hipStream_t stream, Rec** out) {
+  if (m <= 0 || ks.passes == 0) {
+    *out = a;
+    return 0;
+  }
+  if (ks.passes > kMaxPasses) return fail(PDP_ERR_INTERNAL, "too many radix passes");
+  if (ctx->tile_slot + ks.passes > kNumCounters) {
+    HIP_TRY(hipMemsetAsync(counters + kCtrTile0, 0, (kNumCounters - kCtrTile0) * 8, stream));
+    ctx->tile_slot = kCtrTile0;
   }
   HIP_TRY(hipMemsetAsync(hist, 0, kMaxPasses * kHist * 8, stream));
   ProfScope prof_generic(ctx, PDP_STAGE_GENERIC, stream);
@@ -910,16 +937,42 @@ int sort_pid_pk(pdp_ctx* ctx, Rec* a, Rec* b, int64_t m, const Plan& plan, uint6
   for (int p = 0; p < ks.passes; ++p) {
     int rc = next_epoch(ctx, stream, status, status_bytes, ws);
     if (rc) return rc;
-    if (tile_slot0 + p >= (int)kNumCounters) return fail(PDP_ERR_INTERNAL, "too many radix passes");
     hipLaunchKernelGGL(k_onesweep<false>, dim3((unsigned)tiles), dim3(kThreads), 0, stream,
                        (const int64_t*)nullptr, (const int64_t*)nullptr, (const double*)nullptr, src, dst, m,
                        counters, (int)kCtrNGeneric, ks, p, off + p * kHist, status, ctx->epoch, counters,
-                       tile_slot0 + p);
+                       (int)ctx->tile_slot++);
     std::swap(src, dst);
   }
   HIP_TRY(hipGetLastError());
   *out = src;
   return 0;
+}
+
+KeySpec composite_spec(int mode, int hi_bits, int lo_bits, int pkb, uint32_t U, uint32_t P) {
+  KeySpec ks{};
+  ks.mode = mode;
+  ks.low = 0;
+  ks.pkb = pkb;
+  ks.num_pids = U;
+  ks.num_parts = P;
+  // digits of 8 bits; mode 3: lo = 64 bits of val, hi = pid field starting at bit 64
+  int sh = 0, p = 0;
+  const int lo_total = mode == 3 ? 64 : lo_bits + hi_bits;
+  while (sh < lo_total && p < kMaxPasses) {
+    ks.shift[p] = sh;
+    ks.bits[p] = std::min(8, lo_total - sh);
+    sh += ks.bits[p];
+    ++p;
+  }
+  if (mode == 3) {
+    for (int h = 0; h < hi_bits; h += 8) {
+      ks.shift[p] = 64 + h;
+      ks.bits[p] = std::min(8, hi_bits - h);
+      ++p;
+    }
+  }
+  ks.passes = p;
+  return ks;
 }
 
 int run_generic(pdp_ctx* ctx, Rec* sorted, Rec* spare, const std::vector<unsigned long long>& ranges,
@@ -948,41 +1001,72 @@ int run_generic(pdp_ctx* ctx, Rec* sorted, Rec* spare, const std::vector<unsigne
   HIP_TRY(hipFreeAsync(d_rsrc, stream));
   HIP_TRY(hipFreeAsync(d_rdst, stream));
 
+  // 1) rows by (pid, pk), stable (input order within a group)
   Rec* r = nullptr;
-  int rc = sort_pid_pk(ctx, spare, sorted, total, plan, bp->sampling_seed, U, P, hist, off, counters, status,
-                       status_bytes, ws, kCtrTile0 + 16, stream, &r);
+  int rc = sort_recs(ctx, spare, sorted, total, composite_spec(1, plan.pidb, plan.pkb, plan.pkb, U, P), hist, off,
+                     counters, status, status_bytes, ws, stream, &r);
   if (rc) return rc;
+  Rec* r_other = (r == spare) ? sorted : spare;
 
-  long long *gsc, *psc, *gpos, *pfirst;
-  unsigned long long* gcnt;
-  double *gx, *gy;
   const size_t m8 = (size_t)total * 8;
+  long long *gsc, *psc, *gpos, *pfirst;
   HIP_TRY(hipMallocAsync((void**)&gsc, m8, stream));
   HIP_TRY(hipMallocAsync((void**)&psc, m8, stream));
   HIP_TRY(hipMallocAsync((void**)&gpos, m8 + 8, stream));
   HIP_TRY(hipMallocAsync((void**)&pfirst, m8, stream));
-  HIP_TRY(hipMallocAsync((void**)&gcnt, m8, stream));
-  HIP_TRY(hipMallocAsync((void**)&gx, m8, stream));
-  HIP_TRY(hipMallocAsync((void**)&gy, m8, stream));
-  HIP_TRY(hipMemsetAsync(gcnt, 0, m8, stream));
-  HIP_TRY(hipMemsetAsync(gx, 0, m8, stream));
-  HIP_TRY(hipMemsetAsync(gy, 0, m8, stream));
   const int gr = grid_for(total, kThreads);
   hipLaunchKernelGGL(k_stream_flags, dim3(gr), dim3(kThreads), 0, stream, r, total, gsc, psc);
-  rc = scan_inplace(gsc, total, stream);
-  if (rc) return rc;
-  rc = scan_inplace(psc, total, stream);
-  if (rc) return rc;
+  if ((rc = scan_inplace(gsc, total, stream))) return rc;
+  if ((rc = scan_inplace(psc, total, stream))) return rc;
   hipLaunchKernelGGL(k_stream_starts, dim3(gr), dim3(kThreads), 0, stream, gsc, psc, r, total, gpos, pfirst);
-  long long ngroups = 0;
+  long long ngroups = 0, npids = 0;
   HIP_TRY(hipMemcpyAsync(&ngroups, gsc + (total - 1), 8, hipMemcpyDeviceToHost, stream));
-  hipLaunchKernelGGL(k_stream_rows, dim3(gr), dim3(kThreads), 0, stream, r, total, gsc, psc, gpos, pfirst, sp, gcnt,
-                     gx, gy);
+  HIP_TRY(hipMemcpyAsync(&npids, psc + (total - 1), 8, hipMemcpyDeviceToHost, stream));
   HIP_TRY(hipStreamSynchronize(stream));
-  hipLaunchKernelGGL(k_stream_groups, dim3(grid_for(ngroups, kThreads)), dim3(kThreads), 0, stream, r, psc, gpos,
-                     pfirst, (int64_t)ngroups, sp, gcnt, gx, gy, acc);
+
+  // 2) L_inf ranks: sort (group, row priority, row) -> rank within group.
+  Rec *x1, *x2;
+  HIP_TRY(hipMallocAsync((void**)&x1, (size_t)total * sizeof(Rec), stream));
+  HIP_TRY(hipMallocAsync((void**)&x2, (size_t)total * sizeof(Rec), stream));
+  uint8_t* row_keep;
+  int32_t* grank;
+  HIP_TRY(hipMallocAsync((void**)&row_keep, (size_t)total, stream));
+  HIP_TRY(hipMallocAsync((void**)&grank, (size_t)ngroups * 4, stream));
+  hipLaunchKernelGGL(k_stream_row_prio, dim3(gr), dim3(kThreads), 0, stream, r, total, gsc, gpos, sp.seed, x1);
+  Rec* xs = nullptr;
+  const int gbits = std::max(1, pdp::ceil_log2_u64((uint64_t)ngroups));
+  if ((rc = sort_recs(ctx, x1, x2, total, composite_spec(3, gbits, 64, plan.pkb, U, P), hist, off, counters, status,
+                      status_bytes, ws, stream, &xs)))
+    return rc;
+  hipLaunchKernelGGL(k_stream_ranks, dim3(gr), dim3(kThreads), 0, stream, xs, total, gpos, (int64_t)sp.linf,
+                     row_keep, (int32_t*)nullptr);
+  // 3) L0 ranks: sort (pid, group priority, group) -> rank within pid.
+  const int ggr = grid_for(ngroups, kThreads);
+  hipLaunchKernelGGL(k_stream_group_prio, dim3(ggr), dim3(kThreads), 0, stream, r, psc, gpos, (int64_t)ngroups,
+                     sp.seed, x1);
+  const int pbits = std::max(1, pdp::ceil_log2_u64((uint64_t)npids));
+  if ((rc = sort_recs(ctx, x1, x2, ngroups, composite_spec(3, pbits, 64, plan.pkb, U, P), hist, off, counters,
+                      status, status_bytes, ws, stream, &xs)))
+    return rc;
+  hipLaunchKernelGGL(k_stream_ranks, dim3(ggr), dim3(kThreads), 0, stream, xs, (int64_t)ngroups, pfirst,
+                     (int64_t)sp.l0, (uint8_t*)nullptr, grank);
+  // 4) accumulate kept rows per group, emit kept groups.
+  unsigned long long* gcnt;
+  double *gx, *gy;
+  HIP_TRY(hipMallocAsync((void**)&gcnt, (size_t)ngroups * 8, stream));
+  HIP_TRY(hipMallocAsync((void**)&gx, (size_t)ngroups * 8, stream));
+  HIP_TRY(hipMallocAsync((void**)&gy, (size_t)ngroups * 8, stream));
+  HIP_TRY(hipMemsetAsync(gcnt, 0, (size_t)ngroups * 8, stream));
+  HIP_TRY(hipMemsetAsync(gx, 0, (size_t)ngroups * 8, stream));
+  HIP_TRY(hipMemsetAsync(gy, 0, (size_t)ngroups * 8, stream));
+  hipLaunchKernelGGL(k_stream_rows, dim3(gr), dim3(kThreads), 0, stream, r, total, gsc, grank, row_keep, sp, gcnt,
+                     gx, gy);
+  hipLaunchKernelGGL(k_stream_groups, dim3(ggr), dim3(kThreads), 0, stream, r, gpos, grank, (int64_t)ngroups, sp,
+                     gcnt, gx, gy, acc);
   HIP_TRY(hipGetLastError());
-  for (void* p : {(void*)gsc, (void*)psc, (void*)gpos, (void*)pfirst, (void*)gcnt, (void*)gx, (void*)gy})
+  (void)r_other;
+  for (void* p : {(void*)gsc, (void*)psc, (void*)gpos, (void*)pfirst, (void*)x1, (void*)x2, (void*)row_keep,
+                  (void*)grank, (void*)gcnt, (void*)gx, (void*)gy})
     HIP_TRY(hipFreeAsync(p, stream));
   return 0;
 }
@@ -1187,6 +1271,7 @@ int pdp_bound_accumulate(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_
   unsigned long long* ranges = (unsigned long long*)(ws + L.ranges);
   const size_t status_bytes = (size_t)L.tiles * kStatusStride * 8;
   HIP_TRY(hipMemsetAsync(ws + L.hist, 0, L.status - L.hist, stream));  // hist, off, counters
+  ctx->tile_slot = kCtrTile0;
 
   if (bp->bounds_already_enforced) {
     {
@@ -1235,12 +1320,12 @@ int pdp_bound_accumulate(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_
     if (p == 0)
       hipLaunchKernelGGL(k_onesweep<true>, dim3((unsigned)L.tiles), dim3(kThreads), 0, stream, cols->pid, cols->pk,
                          cols->value, (const Rec*)nullptr, dst, n, counters, (int)kCtrNKept, ks, p, off + p * kHist,
-                         status, ctx->epoch, counters, (int)kCtrTile0 + p);
+                         status, ctx->epoch, counters, (int)ctx->tile_slot++);
     else
       hipLaunchKernelGGL(k_onesweep<false>, dim3((unsigned)L.tiles), dim3(kThreads), 0, stream,
                          (const int64_t*)nullptr, (const int64_t*)nullptr, (const double*)nullptr, src, dst, n,
                          counters, (int)kCtrNKept, ks, p, off + p * kHist, status, ctx->epoch, counters,
-                         (int)kCtrTile0 + p);
+                         (int)ctx->tile_slot++);
     src = dst;
     dst = (dst == recs_a) ? recs_b : recs_a;
   }
@@ -1249,11 +1334,13 @@ int pdp_bound_accumulate(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_
   Rec* spare = dst;
 
   OvList ov{ranges, counters};
+  BigList big{(unsigned long long*)(ws + L.big), L.big_cap};
   const int64_t seg_grid = (n + kSegTile - 1) / kSegTile;
   {
     ProfScope ps(ctx, PDP_STAGE_BUCKETS, stream);
     hipLaunchKernelGGL(k_segments, dim3((unsigned)seg_grid), dim3(kThreads), 0, stream, sorted, counters,
-                       (int)kCtrNKept, sp, acc, ov, (int)bp->debug_force_fallback);
+                       (int)kCtrNKept, sp, acc, ov, big, (int)bp->debug_force_fallback);
+    hipLaunchKernelGGL(k_segments_big, dim3(1024), dim3(64 * kBigWaves), 0, stream, sorted, counters, sp, acc, big);
   }
   HIP_TRY(hipGetLastError());
 

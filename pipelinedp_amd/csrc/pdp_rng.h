@@ -2,10 +2,12 @@
 //
 // Bit-for-bit the same specification as oracle/pdp_oracle.py (the CPU
 // checker):
-//   * splitmix64 finaliser, keyed 4-round Feistel bijection on [0, 2^bits),
-//     cycle walking for [0, n) -> uniform sampling without replacement
-//     (replaces np.random.choice in LocalBackend.sample_fixed_per_key,
+//   * splitmix64 priorities ranked per group -> uniform sampling without
+//     replacement (replaces np.random.choice in
+//     LocalBackend.sample_fixed_per_key,
 //     /root/reference/pipeline_dp/pipeline_backend.py:504-520);
+//   * a keyed Feistel bijection (only used to scramble Zipf ranks in the
+//     synthetic generator);
 //   * Philox4x32-10 (Random123) -> uniform doubles in (0,1) -> Laplace by
 //     inverse CDF, Gaussian by Box-Muller.
 // The noise is Philox-based and is NOT PyDP's secure (granularity-rounded)
@@ -42,21 +44,35 @@ PDP_HD uint64_t splitmix64(uint64_t x) {
 
 PDP_HD uint64_t bitmask(int bits) { return bits >= 64 ? ~0ull : ((1ull << bits) - 1ull); }
 
-// Keyed Feistel bijection on [0, 2^bits), bits in [0, 32].
+PDP_HD uint32_t fmix32(uint32_t h) {
+  h ^= h >> 16;
+  h *= 0x85EBCA6Bu;
+  h ^= h >> 13;
+  h *= 0xC2B2AE35u;
+  h ^= h >> 16;
+  return h;
+}
+
+PDP_HD uint32_t mask32(int bits) { return bits >= 32 ? 0xFFFFFFFFu : ((1u << bits) - 1u); }
+
+// Keyed 4-round Feistel bijection on [0, 2^bits), bits in [0, 32]; 32-bit
+// round function F_r(R) = fmix32(R * 0x9E3779B1 + k_r).
 PDP_HD uint32_t perm_bits(uint32_t x, int bits, uint64_t key) {
+  const uint32_t k0 = (uint32_t)key, k1 = (uint32_t)(key >> 32);
+  const uint32_t rk[4] = {k0, k1, k0 ^ 0x85EBCA6Bu, k1 ^ 0xC2B2AE35u};
   const int h1 = (bits + 1) >> 1, h2 = bits >> 1;
   int wl = h1, wr = h2;
-  uint64_t left = (uint64_t)x >> h2, right = (uint64_t)x & bitmask(h2);
+  uint32_t left = h2 >= 32 ? 0u : (x >> h2), right = x & mask32(h2);
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
-    const uint64_t f = splitmix64(key + 0xD1B54A32D192ED03ull * (uint64_t)(r + 1) + right);
-    const uint64_t nl = right;
-    const uint64_t nr = left ^ (f & bitmask(wl));
+    const uint32_t f = fmix32(right * 0x9E3779B1u + rk[r]);
+    const uint32_t nl = right;
+    const uint32_t nr = left ^ (f & mask32(wl));
     left = nl;
     right = nr;
     const int t = wl; wl = wr; wr = t;
   }
-  return (uint32_t)((left << h2) | right);
+  return (left << h2) | right;
 }
 
 PDP_HD int ceil_log2_u64(uint64_t n) {
@@ -77,10 +93,20 @@ PDP_HD uint32_t cycle_walk(uint32_t j, uint64_t n, uint64_t key) {
   return y;
 }
 
-PDP_HD uint64_t pk_perm_key(uint64_t seed, uint64_t pid) { return splitmix64(seed ^ splitmix64(pid + 1ull)); }
+// Contribution-bounding priorities (uniform sampling without replacement by
+// ranking 64-bit hashes; ties broken by pk / input order):
+//   L0:    keep the L0 partitions of a pid with the smallest (group_priority, pk)
+//   L_inf: keep the L_inf rows of a (pid, pk) group with the smallest
+//          (row_priority(gprio, j), j), j = input-order rank within the group.
+PDP_HD uint64_t pid_key(uint64_t seed, uint64_t pid) { return splitmix64(seed ^ splitmix64(pid + 1ull)); }
 
-PDP_HD uint64_t group_perm_key(uint64_t seed, uint64_t pid, uint64_t pk) {
-  return splitmix64(pk_perm_key(seed, pid) ^ splitmix64(pk + 0x632BE59BD9B4E019ull));
+PDP_HD uint64_t group_priority(uint64_t pidkey, uint64_t pk) {
+  return splitmix64(pidkey + (pk + 1ull) * 0xD1B54A32D192ED03ull);
+}
+
+PDP_HD uint64_t row_priority(uint64_t gprio, uint64_t j) {
+  const uint64_t gkey = splitmix64(gprio ^ 0xA0761D6478BD642Full);
+  return splitmix64(gkey + (j + 1ull) * 0x9E3779B97F4A7C15ull);
 }
 
 struct u32x4 { uint32_t x, y, z, w; };

@@ -75,7 +75,7 @@ def test_bound_accumulate_matches_oracle(ex, cfgi, fallback):
     need_val = bool(mask & (2 | 4 | 8))
     _, _, rc, cnt, x, y = run_gpu(ex, pid, pk, val if need_val else None, U, P, bp, mask, seed=77 + cfgi,
                                   fallback=fallback)
-    ref = o.bound_and_accumulate(pid, pk, val if need_val else None, P, bp, "feistel", seed=77 + cfgi)
+    ref = o.bound_and_accumulate(pid, pk, val if need_val else None, P, bp, "hash", seed=77 + cfgi)
     check_acc(ref, rc, cnt, x, y, mask, val)
     if cfgi == 5 and not fallback:
         assert ex.stats().fallback_rows > 0  # huge privacy ids went through the generic path
@@ -87,7 +87,7 @@ def test_dropped_rows_and_public_partitions(ex):
     pk = np.where(pk % 3 == 0, -1, pk)  # non-public rows dropped
     bp = o.BoundParams(3, 2, 0.0, 10.0)
     _, _, rc, cnt, x, _ = run_gpu(ex, pid, pk, val, U, P, bp, 1 | 2 | 16)
-    ref = o.bound_and_accumulate(pid, pk, val, P, bp, "feistel", seed=3)
+    ref = o.bound_and_accumulate(pid, pk, val, P, bp, "hash", seed=3)
     check_acc(ref, rc, cnt, x, None, 1 | 2 | 16, val)
     assert rc[::3].sum() == 0
     pk_all = np.full(n, -1)
@@ -156,7 +156,7 @@ def test_release_matches_oracle(ex, ri):
     pid, pk, val = o.synth_rows(n, U, P, seed=31 + ri, zipf_s=1.1)
     bp = o.BoundParams(3, 2, -1.0, 6.0)
     cfg, acc, *_ = run_gpu(ex, pid, pk, val, U, P, bp, mask, seed=8)
-    ref = o.bound_and_accumulate(pid, pk, val, P, bp, "feistel", seed=8)
+    ref = o.bound_and_accumulate(pid, pk, val, P, bp, "hash", seed=8)
     budgets = {m: (0.3 + 0.1 * i, 1e-7 * (i + 1)) for i, m in enumerate(("count", "sum", "mean", "variance",
                                                                          "privacy_id_count"))}
     slot = {"count": 0, "sum": 1, "mean": 2, "variance": 3, "privacy_id_count": 4}
@@ -236,7 +236,7 @@ def test_engine_columnar_device_input_and_select_partitions():
     sel = engine.select_partitions(data, pdp.SelectPartitionsParams(max_partitions_contributed=3), None)
     acct.compute_budgets()
     out = dict(res)
-    ref = o.bound_and_accumulate(pid, pk, val, P, o.BoundParams(3, 2, 0.0, 10.0), "feistel", seed=4)
+    ref = o.bound_and_accumulate(pid, pk, val, P, o.BoundParams(3, 2, 0.0, 10.0), "hash", seed=4)
     for k, t in out.items():
         assert abs(t.count - ref.count[k]) < 1e-2  # eps = 1e6 / 3 mechanisms: tiny noise
     # huge eps: truncated geometric keeps every partition with >= 2 privacy

@@ -11,7 +11,7 @@ import pdp_oracle as o
 from golden_util import aggregate_cases, encode_case, known_answers, load, sum_tolerance
 
 
-def oracle_run(d, sampler="feistel", seed=0, noise=False):
+def oracle_run(d, sampler="hash", seed=0, noise=False):
     cfg = d["meta"]["cfg"]
     pid, pk, keys = encode_case(d)
     value = d["value"] if len(d["value"]) else None
@@ -128,16 +128,28 @@ def test_feistel_is_bijection():
         assert sorted(y.tolist()) == list(range(n))
 
 
-def test_feistel_sampler_is_uniform():
-    """Inclusion frequency of each row under L_inf sampling ~ L_inf/n."""
-    n, linf, trials = 7, 3, 4000
-    hits = np.zeros(n)
-    for s in range(trials):
-        y = o.cycle_walk(np.arange(n), np.full(n, n), np.full(n, o.group_perm_key(s, 1, 2), dtype=np.uint64))
-        hits += y < linf
-    p = linf / n
-    tol = 4 * math.sqrt(p * (1 - p) / trials)
-    assert np.all(np.abs(hits / trials - p) < tol)
+def test_hash_sampler_is_uniform():
+    """Inclusion frequency of each row of an n-row group under L_inf sampling
+    is L_inf / n, and of each partition under L0 sampling is L0 / R."""
+    trials = 20000
+    for n, linf in ((2, 1), (3, 1), (5, 2), (7, 3), (12, 5)):
+        seeds = np.arange(trials)
+        pid = np.zeros(trials * n, np.int64)
+        gprio = o.group_priority(np.repeat(seeds, n), pid, 2)
+        j = np.tile(np.arange(n), trials)
+        pr = o.row_priority(gprio, j).reshape(trials, n)
+        rank = np.argsort(np.argsort(pr, axis=1, kind="stable"), axis=1, kind="stable")
+        freq = (rank < linf).mean(0)
+        p = linf / n
+        assert np.all(np.abs(freq - p) < 4.5 * math.sqrt(p * (1 - p) / trials)), (n, freq)
+    for R, l0 in ((3, 1), (5, 2), (9, 4)):
+        seeds = np.repeat(np.arange(trials), R)
+        pks = np.tile(np.arange(R), trials)
+        pr = o.group_priority(seeds, np.full(len(pks), 7), pks).reshape(trials, R)
+        rank = np.argsort(np.argsort(pr, axis=1, kind="stable"), axis=1, kind="stable")
+        freq = (rank < l0).mean(0)
+        p = l0 / R
+        assert np.all(np.abs(freq - p) < 4.5 * math.sqrt(p * (1 - p) / trials)), (R, freq)
 
 
 def test_binding_bounds_match_reference_distribution():
@@ -149,7 +161,7 @@ def test_binding_bounds_match_reference_distribution():
     runs = 400
     res = np.zeros((runs, P, 3))
     for s in range(runs):
-        acc = o.bound_and_accumulate(d["pid"], d["pk"], d["value"], P, bp, "feistel", seed=1000 + s)
+        acc = o.bound_and_accumulate(d["pid"], d["pk"], d["value"], P, bp, "hash", seed=1000 + s)
         res[s] = np.stack([acc.count, acc.sum, acc.row_count], 1)
     ref_mean, ref_std = d["mean"], d["std"]
     se = np.sqrt(ref_std**2 / int(d["runs"]) + res.std(0)**2 / runs) + 1e-9
