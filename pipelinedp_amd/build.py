@@ -7,7 +7,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 SRC = os.path.join(HERE, "csrc", "pdp_kernels.hip")
 OUT = os.path.join(HERE, "libpdp_hip.so")
-DEPS = [SRC, os.path.join(HERE, "csrc", "pdp_rng.h"), os.path.join(ROOT, "include", "pdp_hip.h")]
+CSRC = os.path.join(HERE, "csrc")
+DEPS = [os.path.join(CSRC, f) for f in sorted(os.listdir(CSRC))] + [os.path.join(ROOT, "include", "pdp_hip.h")]
 
 
 def build(force: bool = False, verbose: bool = True) -> str:
