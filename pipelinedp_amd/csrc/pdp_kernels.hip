@@ -85,8 +85,11 @@ struct SegParams {
   int has_value;
   double a, b, mid;
   double smin, smax;
-  int debug;  // experiment flags: 1 skip emit, 2 skip sort, 4 skip sampling
+  int packed;  // row_count word holds (count << 32) | row_count until k_unpack_counts
+  int debug;   // experiment flags (bench ablations), kDebugBatchKernel
 };
+
+constexpr int kDebugBatchKernel = 4096;  // use k_segments even when k_lean applies
 
 struct AccPtrs {
   unsigned long long* row_count;
@@ -252,6 +255,7 @@ constexpr uint64_t kFlagAgg = 1ull << 46;
 constexpr uint64_t kFlagPre = 2ull << 46;
 constexpr uint64_t kFlagMask = 3ull << 46;
 constexpr uint64_t kValMask = (1ull << 46) - 1ull;
+constexpr int kLookback = 8;
 
 template <bool SOA>
 __global__ __launch_bounds__(kThreads, 2) void k_onesweep(
@@ -353,23 +357,39 @@ __global__ __launch_bounds__(kThreads, 2) void k_onesweep(
       __hip_atomic_store(&st[t], ep | kFlagPre | (uint64_t)tcount, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     } else {
       __hip_atomic_store(&st[t], ep | kFlagAgg | (uint64_t)tcount, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      // Look back kLookback predecessors per round trip (independent loads in
+      // flight), consuming them nearest-first up to the first inclusive
+      // prefix or the first one not published yet.
       int64_t j = tile - 1;
       unsigned int spins = 0;
       while (true) {
-        const uint64_t s = __hip_atomic_load(&status[(size_t)j * kStatusStride + t], __ATOMIC_RELAXED,
-                                             __HIP_MEMORY_SCOPE_AGENT);
-        const uint64_t f = s & kFlagMask;
-        if ((s >> 48) == (uint64_t)epoch && f != 0) {
-          excl += s & kValMask;
-          if (f == kFlagPre) break;
-          --j;
-          continue;
+        uint64_t sv[kLookback];
+#pragma unroll
+        for (int w = 0; w < kLookback; ++w)
+          sv[w] = j - w >= 0 ? __hip_atomic_load(&status[(size_t)(j - w) * kStatusStride + t], __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT)
+                             : 0ull;
+        int used = 0;
+        bool done = false;
+#pragma unroll
+        for (int w = 0; w < kLookback; ++w) {
+          const uint64_t s = sv[w];
+          const uint64_t f = s & kFlagMask;
+          if (!done && used == w && (s >> 48) == (uint64_t)epoch && f != 0) {
+            excl += s & kValMask;
+            used = w + 1;
+            done = f == kFlagPre;
+          }
         }
-        if (++spins > (1u << 24)) {
-          atomicOr(&counters[kCtrErr], 1ull);
-          break;
+        if (done) break;
+        j -= used;
+        if (used == 0) {
+          if (++spins > (1u << 24)) {
+            atomicOr(&counters[kCtrErr], 1ull);
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
         }
-        __builtin_amdgcn_s_sleep(1);
       }
       __hip_atomic_store(&st[t], ep | kFlagPre | (excl + tcount), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
@@ -426,8 +446,13 @@ __device__ __forceinline__ void row_terms(const SegParams& sp, double v, double&
 
 __device__ __forceinline__ void emit_group(const SegParams& sp, const AccPtrs& acc, uint32_t pk, uint32_t cnt,
                                            double x, double y) {
-  atomicAdd(&acc.row_count[pk], 1ull);
-  if (sp.want_count) atomicAdd(&acc.count[pk], (unsigned long long)cnt);
+  if (sp.packed) {
+    // one 64-bit atomic for (count, row_count); both stay < 2^32 (rows < 2^32)
+    atomicAdd(&acc.row_count[pk], ((unsigned long long)cnt << 32) | 1ull);
+  } else {
+    atomicAdd(&acc.row_count[pk], 1ull);
+    if (sp.want_count) atomicAdd(&acc.count[pk], (unsigned long long)cnt);
+  }
   if (sp.xmode != kXNone) {
     if (sp.xmode == kXRawSum) x = clip(x, sp.smin, sp.smax);  // combiners.py:256-259
     atomicAdd(&acc.x[pk], x);
@@ -593,6 +618,16 @@ __global__ void k_enforced(const int64_t* __restrict__ pk, const double* __restr
     emit_group(sp, acc, (uint32_t)b, 1u, x, y);
   }
   if (invalid) atomicAdd(&counters[kCtrInvalid], (unsigned long long)invalid);
+}
+
+// Packed (count << 32 | row_count) words -> the two int64 accumulators.
+__global__ void k_unpack_counts(unsigned long long* __restrict__ row_count, unsigned long long* __restrict__ count,
+                                int64_t P) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < P; i += (int64_t)gridDim.x * blockDim.x) {
+    const unsigned long long v = row_count[i];
+    row_count[i] = v & 0xFFFFFFFFull;
+    count[i] = v >> 32;
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -771,7 +806,7 @@ Layout layout_for(int64_t n) {
   L.tiles = (std::max<int64_t>(n, 1) + kTile - 1) / kTile;
   L.status = o; o += align_up((size_t)L.tiles * kStatusStride * 8, 256);
   L.ranges = o; o += align_up((size_t)kOverflowCap * 16, 256);
-  L.big_cap = (uint64_t)std::max<int64_t>(n, 1) / (kSmallMax + 1) + 64;
+  L.big_cap = (uint64_t)std::max<int64_t>(n, 1) / 129 + 64;  // segments / batches of > 128 rows
   L.big = o; o += align_up((size_t)L.big_cap * 16, 256);
   L.total = o;
   return L;
@@ -823,6 +858,7 @@ SegParams make_seg(const pdp_bound_params* bp, int low, int pkb, bool has_value)
   sp.mid = bp->min_value + (bp->max_value - bp->min_value) / 2;  // dp_computations.py:65-69
   sp.smin = bp->min_sum_per_partition;
   sp.smax = bp->max_sum_per_partition;
+  sp.packed = 0;
   sp.debug = bp->reserved;
   return sp;
 }
@@ -1287,6 +1323,7 @@ int pdp_bound_accumulate(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_
     return 0;
   }
 
+  sp.packed = sp.want_count && n < (1ll << 32);
   KeySpec ks{};
   ks.mode = 0;
   ks.low = plan.low;
@@ -1338,8 +1375,14 @@ int pdp_bound_accumulate(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_
   const int64_t seg_grid = (n + kSegTile - 1) / kSegTile;
   {
     ProfScope ps(ctx, PDP_STAGE_BUCKETS, stream);
-    hipLaunchKernelGGL(k_segments, dim3((unsigned)seg_grid), dim3(kThreads), 0, stream, sorted, counters,
-                       (int)kCtrNKept, sp, acc, ov, big, (int)bp->debug_force_fallback);
+    if (bp->max_partitions_contributed <= kLeanMaxL0 && !(sp.debug & kDebugBatchKernel)) {
+      const int64_t waves = (n + kLeanChunk - 1) / kLeanChunk;
+      hipLaunchKernelGGL(k_lean, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, stream, sorted, counters,
+                         (int)kCtrNKept, sp, acc, ov, big, (int)bp->debug_force_fallback);
+    } else {
+      hipLaunchKernelGGL(k_segments, dim3((unsigned)seg_grid), dim3(kThreads), 0, stream, sorted, counters,
+                         (int)kCtrNKept, sp, acc, ov, big, (int)bp->debug_force_fallback);
+    }
     hipLaunchKernelGGL(k_segments_big, dim3(1024), dim3(64 * kBigWaves), 0, stream, sorted, counters, sp, acc, big);
   }
   HIP_TRY(hipGetLastError());
@@ -1371,6 +1414,11 @@ int pdp_bound_accumulate(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_
     HIP_TRY(hipMemcpyAsync(&err, counters + kCtrErr, 8, hipMemcpyDeviceToHost, stream));
     HIP_TRY(hipStreamSynchronize(stream));
     if (err) return fail(PDP_ERR_INTERNAL, "radix look-back timed out (generic path)");
+  }
+  if (sp.packed) {
+    hipLaunchKernelGGL(k_unpack_counts, dim3(grid_for(P, kThreads, 4096)), dim3(kThreads), 0, stream, acc.row_count,
+                       acc.count, P);
+    HIP_TRY(hipGetLastError());
   }
   return 0;
 }

@@ -28,12 +28,15 @@ def _dev(a, torch):
     return None if a is None else torch.from_numpy(np.ascontiguousarray(a)).cuda()
 
 
-def run_gpu(ex, pid, pk, val, U, P, bp: o.BoundParams, mask, seed=3, fallback=False):
+BATCH_KERNEL = 4096  # debug flag: k_segments (register bitonic batches) instead of k_lean
+
+
+def run_gpu(ex, pid, pk, val, U, P, bp: o.BoundParams, mask, seed=3, fallback=False, debug_flags=0):
     import torch
     from pipelinedp_amd.executor import BoundConfig
     cfg = BoundConfig(mask, bp.max_partitions_contributed, bp.max_contributions_per_partition, bp.min_value,
                       bp.max_value, bp.min_sum_per_partition, bp.max_sum_per_partition,
-                      bp.contribution_bounds_already_enforced, seed, fallback)
+                      bp.contribution_bounds_already_enforced, seed, fallback, debug_flags)
     acc = ex.accumulate(_dev(pid, torch), _dev(pk, torch), _dev(val, torch), U, P, cfg)
     torch.cuda.synchronize()
     g = lambda t: None if t is None else t.cpu().numpy()  # noqa: E731
@@ -63,21 +66,24 @@ CONFIGS = [
     (25000, 3, 7, 0.0, 2, 5, (1.0, 5.0), None, 1 | 2 | 4 | 16),  # pids with > 2048 rows -> generic path
     (5000, 5000, 1, 0.0, 1, 1, (0.0, 1.0), None, 1 | 2),  # one partition
     (4000, 1, 3000, 1.1, 7, 2, (0.0, 10.0), None, 1 | 4 | 16),  # one privacy id
+    (60000, 400, 5000, 1.1, 4, 2, (0.0, 10.0), None, 1 | 2 | 4),  # ~150 rows / pid: lean + big-batch kernels
+    (40000, 2000, 300, 1.3, 16, 1, (0.0, 5.0), None, 1 | 4 | 8 | 16),  # largest L0 of the lean kernel
+    (30000, 1000, 3, 0.0, 2, 8, (0.0, 10.0), None, 1 | 2),  # groups of > 4 kept rows (wave-sum path)
 ]
 
 
-@pytest.mark.parametrize("fallback", [False, True])
+@pytest.mark.parametrize("mode", ["lean", "batch", "fallback"])
 @pytest.mark.parametrize("cfgi", range(len(CONFIGS)))
-def test_bound_accumulate_matches_oracle(ex, cfgi, fallback):
+def test_bound_accumulate_matches_oracle(ex, cfgi, mode):
     n, U, P, z, L0, Linf, vb, pb, mask = CONFIGS[cfgi]
     pid, pk, val = o.synth_rows(n, U, P, seed=100 + cfgi, zipf_s=z, value_lo=-5, value_hi=15)
     bp = o.BoundParams(L0, Linf, *(vb or (None, None)), *(pb or (None, None)))
     need_val = bool(mask & (2 | 4 | 8))
     _, _, rc, cnt, x, y = run_gpu(ex, pid, pk, val if need_val else None, U, P, bp, mask, seed=77 + cfgi,
-                                  fallback=fallback)
+                                  fallback=mode == "fallback", debug_flags=BATCH_KERNEL if mode == "batch" else 0)
     ref = o.bound_and_accumulate(pid, pk, val if need_val else None, P, bp, "hash", seed=77 + cfgi)
     check_acc(ref, rc, cnt, x, y, mask, val)
-    if cfgi == 5 and not fallback:
+    if cfgi == 5 and mode != "fallback":
         assert ex.stats().fallback_rows > 0  # huge privacy ids went through the generic path
 
 
