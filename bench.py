@@ -182,6 +182,9 @@ def main():
             "sort_passes": int(st.sort_passes), "bucket_low_bits": int(st.bucket_low_bits),
             "fallback_rows": int(st.fallback_rows),
         }
+        if st.sweep_tiles:
+            line["sweep_cycles_per_tile"] = {k: round(st.sweep_cycles[i] / st.sweep_tiles)
+                                             for i, k in enumerate(("load_rank", "lookback", "scatter"))}
         print(json.dumps(line), flush=True)
     if world is not None:
         dist.destroy_process_group()

@@ -199,6 +199,8 @@ typedef struct pdp_stats {
   int64_t fallback_ranges;
   int32_t sort_passes;
   int32_t bucket_low_bits;
+  int64_t sweep_cycles[3];     /* radix passes, debug stamps only: load+rank, look-back, scatter */
+  int64_t sweep_tiles;
 } pdp_stats;
 int pdp_get_stats(pdp_ctx* ctx, pdp_stats* out);
 

@@ -48,6 +48,8 @@ enum Counter {
   kCtrNGeneric = 5,
   kCtrNBig = 6,
   kCtrBigNext = 7,
+  kCtrSweepCycles = 8,  // 8..10: onesweep load+rank / look-back / scatter cycles (profiling)
+  kCtrSweepTiles = 11,
   kCtrTile0 = 16,  // 16..63 tile claim counters, one per onesweep launch
 };
 
@@ -67,6 +69,7 @@ struct KeySpec {
   uint64_t seed;
   uint32_t num_pids;
   uint32_t num_parts;
+  int prof;  // accumulate per-phase s_memtime cycles of k_onesweep (kDebugSweepStamps)
 };
 
 // How a row's value feeds the accumulators (combiners.py:254-261, 305-311,
@@ -90,6 +93,7 @@ struct SegParams {
 };
 
 constexpr int kDebugBatchKernel = 4096;  // use k_segments even when k_lean applies
+constexpr int kDebugSweepStamps = 8192;  // per-phase cycle stamps in k_onesweep -> pdp_stats
 
 struct AccPtrs {
   unsigned long long* row_count;
@@ -257,15 +261,21 @@ constexpr uint64_t kFlagMask = 3ull << 46;
 constexpr uint64_t kValMask = (1ull << 46) - 1ull;
 constexpr int kLookback = 8;
 
+// LDS per block ~39 KB (half-tile record staging, digits recomputed from the
+// staged record) and <= 128 VGPRs, so 4 blocks (16 waves) share a CU: the
+// per-tile latency chain (tile claim, loads, look-back) is hidden by the
+// other blocks instead of idling the CU.
+constexpr int kHalfTile = kTile / 2;
+constexpr uint32_t kNoPos = 0xFFFFu;
+
 template <bool SOA>
-__global__ __launch_bounds__(kThreads, 2) void k_onesweep(
+__global__ __launch_bounds__(kThreads, 3) void k_onesweep(
     const int64_t* __restrict__ pid, const int64_t* __restrict__ pk, const double* __restrict__ val,
     const Rec* __restrict__ rin, Rec* __restrict__ rout, int64_t n_in,
     const unsigned long long* __restrict__ counters_n, int n_slot, KeySpec ks, int pass,
     const unsigned long long* __restrict__ off, unsigned long long* __restrict__ status, uint32_t epoch,
     unsigned long long* __restrict__ counters, int tile_slot) {
-  __shared__ Rec s_rec[kTile];
-  __shared__ uint16_t s_dig[kTile];
+  __shared__ Rec s_rec[kHalfTile];
   __shared__ unsigned int s_cnt[4][kHist + 1];
   __shared__ unsigned int s_dstart[256];
   __shared__ long long s_gbase[256];
@@ -274,6 +284,7 @@ __global__ __launch_bounds__(kThreads, 2) void k_onesweep(
   __shared__ unsigned int s_total;
 
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const long long c0 = ks.prof ? (long long)__builtin_amdgcn_s_memtime() : 0;
   if (t == 0) s_tile = (unsigned int)atomicAdd(&counters[tile_slot], 1ull);
   for (int i = t; i < 4 * (kHist + 1); i += kThreads) (&s_cnt[0][0])[i] = 0;
   __syncthreads();
@@ -285,8 +296,7 @@ __global__ __launch_bounds__(kThreads, 2) void k_onesweep(
   const int radix = 1 << radix_bits;
 
   Rec r[kItems];
-  uint32_t dg[kItems];
-  uint32_t rk[kItems];
+  uint32_t dr[kItems];  // digit (9 bits) | rank in wave << 9; later the sorted position
   const int64_t base = tile_start + (int64_t)wave * (kItems * 64) + lane;
 #pragma unroll
   for (int k = 0; k < kItems; ++k) {
@@ -307,14 +317,14 @@ __global__ __launch_bounds__(kThreads, 2) void k_onesweep(
         d = digit_of(ks, pass, r[k]);
       }
     }
-    dg[k] = d;
+    dr[k] = d;
   }
 
   // Wave-level multisplit ranking (stable: item order = wave, k, lane).
   const uint64_t lt = (1ull << lane) - 1ull;
 #pragma unroll
   for (int k = 0; k < kItems; ++k) {
-    const uint32_t d = dg[k];
+    const uint32_t d = dr[k];
     uint64_t peers = ~0ull;
 #pragma unroll
     for (int b = 0; b < 9; ++b) {
@@ -328,26 +338,27 @@ __global__ __launch_bounds__(kThreads, 2) void k_onesweep(
     __builtin_amdgcn_wave_barrier();
     if (before == 0) s_cnt[wave][d] = basec + c;
     __builtin_amdgcn_wave_barrier();
-    rk[k] = basec + before;
+    dr[k] = d | ((basec + before) << 9);
   }
   __syncthreads();
 
   // Per-digit tile counts, per-wave exclusive offsets, digit starts.
   unsigned int tcount = 0;
   {
-    const unsigned int c0 = s_cnt[0][t], c1 = s_cnt[1][t], c2 = s_cnt[2][t], c3 = s_cnt[3][t];
-    tcount = c0 + c1 + c2 + c3;
+    const unsigned int c0w = s_cnt[0][t], c1w = s_cnt[1][t], c2w = s_cnt[2][t], c3w = s_cnt[3][t];
+    tcount = c0w + c1w + c2w + c3w;
     __syncthreads();
     s_cnt[0][t] = 0;
-    s_cnt[1][t] = c0;
-    s_cnt[2][t] = c0 + c1;
-    s_cnt[3][t] = c0 + c1 + c2;
+    s_cnt[1][t] = c0w;
+    s_cnt[2][t] = c0w + c1w;
+    s_cnt[3][t] = c0w + c1w + c2w;
   }
   unsigned int total;
   const unsigned int dstart = block_excl_scan(tcount, s_tmp, total);
   s_dstart[t] = dstart;
   if (t == 0) s_total = total;
 
+  const long long c1 = ks.prof ? (long long)__builtin_amdgcn_s_memtime() : 0;
   // Decoupled look-back per digit.
   if (t < radix) {
     unsigned long long* st = status + (size_t)tile * kStatusStride;
@@ -396,22 +407,37 @@ __global__ __launch_bounds__(kThreads, 2) void k_onesweep(
     s_gbase[t] = (long long)off[t] + (long long)excl - (long long)dstart;
   }
   __syncthreads();
+  const long long c2 = ks.prof ? (long long)__builtin_amdgcn_s_memtime() : 0;
 
-  // Scatter into LDS in digit order, then write contiguous digit runs.
+  // Sorted position of every item in the tile.
 #pragma unroll
   for (int k = 0; k < kItems; ++k) {
-    const uint32_t d = dg[k];
-    if (d < 256) {
-      const uint32_t pos = s_dstart[d] + s_cnt[wave][d] + rk[k];
-      s_rec[pos] = r[k];
-      s_dig[pos] = (uint16_t)d;
-    }
+    const uint32_t d = dr[k] & 511u;
+    dr[k] = d < 256 ? s_dstart[d] + s_cnt[wave][d] + (dr[k] >> 9) : kNoPos;
   }
-  __syncthreads();
+  // Two halves: stage positions [h, h + kHalfTile) in LDS, write contiguous
+  // digit runs (the digit is recomputed from the staged record).
   const unsigned int tot = s_total;
-  for (unsigned int i = t; i < tot; i += kThreads) {
-    const uint32_t d = s_dig[i];
-    rout[s_gbase[d] + (long long)i] = s_rec[i];
+  for (unsigned int h = 0; h < tot; h += kHalfTile) {
+#pragma unroll
+    for (int k = 0; k < kItems; ++k) {
+      const uint32_t q = dr[k] - h;
+      if (q < (uint32_t)kHalfTile) s_rec[q] = r[k];
+    }
+    __syncthreads();
+    const unsigned int e = tot - h < (unsigned int)kHalfTile ? tot - h : (unsigned int)kHalfTile;
+    for (unsigned int i = t; i < e; i += kThreads) {
+      const Rec rc = s_rec[i];
+      rout[s_gbase[digit_of(ks, pass, rc)] + (long long)(h + i)] = rc;
+    }
+    __syncthreads();
+  }
+  if (ks.prof && t == 0) {
+    const long long c3 = (long long)__builtin_amdgcn_s_memtime();
+    atomicAdd(&counters[kCtrSweepCycles], (unsigned long long)(c1 - c0));
+    atomicAdd(&counters[kCtrSweepCycles + 1], (unsigned long long)(c2 - c1));
+    atomicAdd(&counters[kCtrSweepCycles + 2], (unsigned long long)(c3 - c2));
+    atomicAdd(&counters[kCtrSweepTiles], 1ull);
   }
   (void)radix_bits;
 }
@@ -1341,6 +1367,7 @@ int pdp_bound_accumulate(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_
     }
   }
   ctx->stats.sort_passes = plan.passes;
+  ks.prof = (sp.debug & kDebugSweepStamps) != 0;
   {
     ProfScope ps(ctx, PDP_STAGE_HISTOGRAM, stream);
     hipLaunchKernelGGL(k_histogram<true>, dim3(grid_for(n, kThreads, 2048)), dim3(kThreads), 0, stream, cols->pid,
@@ -1387,10 +1414,12 @@ int pdp_bound_accumulate(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_
   }
   HIP_TRY(hipGetLastError());
 
-  unsigned long long host_ctr[8];
+  unsigned long long host_ctr[12];
   HIP_TRY(hipMemcpyAsync(host_ctr, counters, sizeof(host_ctr), hipMemcpyDeviceToHost, stream));
   HIP_TRY(hipStreamSynchronize(stream));
   ctx->stats.kept_rows_in = (int64_t)host_ctr[kCtrNKept];
+  for (int i = 0; i < 3; ++i) ctx->stats.sweep_cycles[i] = (int64_t)host_ctr[kCtrSweepCycles + i];
+  ctx->stats.sweep_tiles = (int64_t)host_ctr[kCtrSweepTiles];
   if (host_ctr[kCtrErr]) return fail(PDP_ERR_INTERNAL, "radix look-back timed out");
   if (host_ctr[kCtrInvalid]) return fail(PDP_ERR_OUT_OF_RANGE, "privacy id or partition id out of range");
   std::vector<unsigned long long> rg;

@@ -8,7 +8,7 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libpdp_hip.so")
+LIB_PATH = os.environ.get("PDP_HIP_LIB") or os.path.join(_HERE, "libpdp_hip.so")  # env: experiment builds
 
 PDP_OK = 0
 METRIC_COUNT, METRIC_SUM, METRIC_MEAN, METRIC_VARIANCE, METRIC_PRIVACY_ID_COUNT = 1, 2, 4, 8, 16
@@ -56,7 +56,8 @@ class Outputs(ctypes.Structure):
 
 class Stats(ctypes.Structure):
     _fields_ = [("kept_rows_in", c_i64), ("fallback_rows", c_i64), ("fallback_ranges", c_i64),
-                ("sort_passes", c_i32), ("bucket_low_bits", c_i32)]
+                ("sort_passes", c_i32), ("bucket_low_bits", c_i32), ("sweep_cycles", c_i64 * 3),
+                ("sweep_tiles", c_i64)]
 
 
 # Every symbol declared in include/pdp_hip.h: (name, restype, argtypes).
