@@ -52,6 +52,26 @@ def stage_bytes(stage, n_in, n_kept, P, nfields):
     }.get(stage)
 
 
+def copy_peak_gbs(torch, nbytes=8 << 30, iters=5):
+    """Achievable HBM ceiling on this box: a device-to-device copy of
+    `nbytes` (read + write bytes / time), the measured counterpart of the
+    8 TB/s spec peak."""
+    src = torch.empty(nbytes // 8, dtype=torch.int64, device="cuda")
+    dst = torch.empty_like(src)
+    dst.copy_(src)
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(iters):
+        dst.copy_(src)
+    b.record()
+    torch.cuda.synchronize()
+    gbs = 2 * nbytes * iters / (a.elapsed_time(b) * 1e-3) / 1e9
+    del src, dst
+    torch.cuda.empty_cache()
+    return round(gbs, 1)
+
+
 def cpu_baseline(args, P):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pdp_oracle as o  # checker / baseline only
@@ -162,6 +182,9 @@ def main():
                 stages[s]["achieved_GBs"] = round(bs / (stages[s]["ms_per_launch"] * 1e-3) / 1e9, 1)
 
     rows_per_s = n * world_size * args.steps / elapsed
+    copy_gbs = copy_peak_gbs(torch) if rank == 0 and not args.no_profile else None
+    if roofline is not None:
+        roofline["copy_peak_measured"] = copy_gbs
     cpu = None
     if rank == 0 and world_size == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args, P)
@@ -184,7 +207,7 @@ def main():
         }
         if st.sweep_tiles:
             line["sweep_cycles_per_tile"] = {k: round(st.sweep_cycles[i] / st.sweep_tiles)
-                                             for i, k in enumerate(("load_rank", "lookback", "scatter"))}
+                                             for i, k in enumerate(("load", "rank", "lookback", "scatter"))}
         print(json.dumps(line), flush=True)
     if world is not None:
         dist.destroy_process_group()

@@ -199,7 +199,7 @@ typedef struct pdp_stats {
   int64_t fallback_ranges;
   int32_t sort_passes;
   int32_t bucket_low_bits;
-  int64_t sweep_cycles[3];     /* radix passes, debug stamps only: load+rank, look-back, scatter */
+  int64_t sweep_cycles[4];     /* radix passes, debug stamps only: load, rank, look-back/bases, scatter */
   int64_t sweep_tiles;
 } pdp_stats;
 int pdp_get_stats(pdp_ctx* ctx, pdp_stats* out);
@@ -214,7 +214,8 @@ enum {
   PDP_STAGE_GENERIC = 4,         /* KF (fallback) */
   PDP_STAGE_RELEASE = 5,         /* K5/K6 */
   PDP_STAGE_ENFORCED = 6,        /* bounds already enforced accumulate */
-  PDP_NUM_STAGES = 7,
+  PDP_STAGE_TILE_COUNTS = 7,     /* K1u per-tile digit counts (passes >= 1) + tile-offset scans */
+  PDP_NUM_STAGES = 8,
 };
 int pdp_profile_enable(pdp_ctx* ctx, int enable);
 /* Waits for recorded events; adds into ms_out/launches_out[PDP_NUM_STAGES]

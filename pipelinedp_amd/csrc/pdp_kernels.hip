@@ -31,7 +31,19 @@
 namespace {
 
 constexpr int kThreads = 256;
-constexpr int kItems = 16;                   // rows per thread in a radix tile
+#ifndef PDP_OS_ITEMS
+#define PDP_OS_ITEMS 16
+#endif
+#ifndef PDP_OS_OCC
+#define PDP_OS_OCC 3
+#endif
+#ifndef PDP_OS_RANK_ATOMIC
+#define PDP_OS_RANK_ATOMIC 0
+#endif
+#ifndef PDP_OS_STAGE_DIV
+#define PDP_OS_STAGE_DIV 2
+#endif
+constexpr int kItems = PDP_OS_ITEMS;         // rows per thread in a radix tile
 constexpr int kTile = kThreads * kItems;     // 4096 rows per radix tile
 constexpr int kMaxPasses = 12;
 constexpr int kHist = 257;                   // 256 digits + drop bucket
@@ -48,8 +60,8 @@ enum Counter {
   kCtrNGeneric = 5,
   kCtrNBig = 6,
   kCtrBigNext = 7,
-  kCtrSweepCycles = 8,  // 8..10: onesweep load+rank / look-back / scatter cycles (profiling)
-  kCtrSweepTiles = 11,
+  kCtrSweepCycles = 8,  // 8..11: onesweep load / rank / look-back / scatter cycles (profiling)
+  kCtrSweepTiles = 12,
   kCtrTile0 = 16,  // 16..63 tile claim counters, one per onesweep launch
 };
 
@@ -58,6 +70,40 @@ struct __align__(16) Rec {
   uint32_t pk;
   double val;
 };
+
+#ifndef PDP_OS_NT
+#define PDP_OS_NT 0
+#endif
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+// 16-byte record load / store of the radix passes (streamed once: optionally
+// non-temporal so they do not displace the L2's working set).
+__device__ __forceinline__ Rec ld_rec(const Rec* p) {
+#if PDP_OS_NT & 1
+  const u32x4 v = __builtin_nontemporal_load((const u32x4*)p);
+  Rec r;
+  r.pid = v.x;
+  r.pk = v.y;
+  r.val = __longlong_as_double((long long)(((uint64_t)v.w << 32) | v.z));
+  return r;
+#else
+  return *p;
+#endif
+}
+
+__device__ __forceinline__ void st_rec(Rec* p, const Rec& r) {
+#if PDP_OS_NT & 2
+  const uint64_t b = (uint64_t)__double_as_longlong(r.val);
+  u32x4 v;
+  v.x = r.pid;
+  v.y = r.pk;
+  v.z = (unsigned int)b;
+  v.w = (unsigned int)(b >> 32);
+  __builtin_nontemporal_store(v, (u32x4*)p);
+#else
+  *p = r;
+#endif
+}
 
 struct KeySpec {
   int mode;  // 0: key = pid >> low ; 1: key = (pid << pkb) | pk ; 3: key = (pid, bits(val)) 96-bit
@@ -70,6 +116,7 @@ struct KeySpec {
   uint32_t num_pids;
   uint32_t num_parts;
   int prof;  // accumulate per-phase s_memtime cycles of k_onesweep (kDebugSweepStamps)
+  int ablate;  // kDebugNoLookback / kDebugLinearWrite (timing ablations, results invalid)
 };
 
 // How a row's value feeds the accumulators (combiners.py:254-261, 305-311,
@@ -94,6 +141,14 @@ struct SegParams {
 
 constexpr int kDebugBatchKernel = 4096;  // use k_segments even when k_lean applies
 constexpr int kDebugSweepStamps = 8192;  // per-phase cycle stamps in k_onesweep -> pdp_stats
+// Timing ablations of the radix passes (bench experiments only; accumulators
+// are left zero): stop after the sort, skip the look-back (prefix 0), write
+// each tile back to its own rows instead of scattering digit runs.
+constexpr int kDebugSortOnly = 16384;
+constexpr int kDebugNoLookback = 32768;
+constexpr int kDebugLinearWrite = 65536;
+constexpr int kDebugLookback = 131072;  // radix passes by decoupled look-back instead of reduce-then-scan
+constexpr int kDebugNoAtomics = 262144;  // K2 skips its accumulator atomics (timing ablation)
 
 struct AccPtrs {
   unsigned long long* row_count;
@@ -235,6 +290,124 @@ __global__ __launch_bounds__(kThreads) void k_histogram(const int64_t* __restric
   if (invalid) atomicAdd(&counters[kCtrInvalid], (unsigned long long)invalid);
 }
 
+// K0 (tile form): the same histograms, plus the pass-0 digit count of every
+// 4096-row input tile (tile_cnt[tile][256], u32) for the reduce-then-scan
+// radix pass.  Blocks stride over whole tiles.
+__global__ __launch_bounds__(kThreads) void k_histogram_tiles(const int64_t* __restrict__ pid,
+                                                              const int64_t* __restrict__ pk, int64_t n,
+                                                              KeySpec ks, unsigned long long* __restrict__ hist,
+                                                              unsigned int* __restrict__ tile_cnt,
+                                                              unsigned long long* __restrict__ counters) {
+  __shared__ unsigned int sh[kMaxPasses * kHist];
+  __shared__ unsigned int st[256];
+  const int t = threadIdx.x;
+  for (int i = t; i < kMaxPasses * kHist; i += kThreads) sh[i] = 0;
+  st[t] = 0;
+  __syncthreads();
+  unsigned int invalid = 0;
+  const int64_t tiles = (n + kTile - 1) / kTile;
+  for (int64_t tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
+    const int64_t base = tile * kTile + t;
+#pragma unroll 4
+    for (int k = 0; k < kItems; ++k) {
+      const int64_t i = base + (int64_t)k * kThreads;
+      if (i >= n) break;
+      const int64_t a = pid[i], b = pk[i];
+      if (b < 0 || b >= (int64_t)ks.num_parts || a < 0 || a >= (int64_t)ks.num_pids) {
+        if (b >= 0) ++invalid;
+        atomicAdd(&sh[256], 1u);
+        continue;
+      }
+      Rec r;
+      r.pid = (uint32_t)a;
+      r.pk = (uint32_t)b;
+      r.val = 0.0;
+      const uint32_t d0 = digit_of(ks, 0, r);
+      atomicAdd(&sh[d0], 1u);
+      atomicAdd(&st[d0], 1u);
+      for (int p = 1; p < ks.passes; ++p) atomicAdd(&sh[p * kHist + digit_of(ks, p, r)], 1u);
+    }
+    __syncthreads();
+    tile_cnt[tile * 256 + t] = st[t];
+    st[t] = 0;
+    __syncthreads();
+  }
+  for (int i = t; i < ks.passes * kHist; i += kThreads)
+    if (sh[i]) atomicAdd(&hist[i], (unsigned long long)sh[i]);
+  if (invalid) atomicAdd(&counters[kCtrInvalid], (unsigned long long)invalid);
+}
+
+// K1u (upsweep of a records pass): digit count of every tile of `rin`.
+__global__ __launch_bounds__(kThreads) void k_tile_counts(const Rec* __restrict__ rin,
+                                                          const unsigned long long* __restrict__ counters_n,
+                                                          int n_slot, KeySpec ks, int pass, int64_t tiles,
+                                                          unsigned int* __restrict__ tile_cnt) {
+  __shared__ unsigned int st[256];
+  const int t = threadIdx.x;
+  st[t] = 0;
+  __syncthreads();
+  const int64_t n = (int64_t)counters_n[n_slot];
+  for (int64_t tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
+    const int64_t base = tile * kTile + t;
+#pragma unroll 4
+    for (int k = 0; k < kItems; ++k) {
+      const int64_t i = base + (int64_t)k * kThreads;
+      if (i < n) atomicAdd(&st[digit_of(ks, pass, rin[i])], 1u);
+    }
+    __syncthreads();
+    tile_cnt[tile * 256 + t] = st[t];
+    st[t] = 0;
+    __syncthreads();
+  }
+}
+
+// Tile-offset scan, step 1: per chunk of kScanTiles tiles, the digit sums.
+constexpr int kScanTiles = 256;
+__global__ __launch_bounds__(kThreads) void k_tile_chunk_sums(const unsigned int* __restrict__ tile_cnt,
+                                                              int64_t tiles, unsigned int* __restrict__ chunk) {
+  const int t = threadIdx.x;
+  const int64_t t0 = (int64_t)blockIdx.x * kScanTiles;
+  const int64_t t1 = t0 + kScanTiles < tiles ? t0 + kScanTiles : tiles;
+  unsigned int s = 0;
+#pragma unroll 8
+  for (int64_t i = t0; i < t1; ++i) s += tile_cnt[i * 256 + t];
+  chunk[(int64_t)blockIdx.x * 256 + t] = s;
+}
+
+// Step 2 (one block per digit): exclusive scan of the chunk sums of digit d,
+// plus the global digit start off[d].
+__global__ __launch_bounds__(kThreads) void k_tile_chunk_scan(unsigned int* __restrict__ chunk, int64_t nchunks,
+                                                              const unsigned long long* __restrict__ off) {
+  __shared__ unsigned int s_tmp[4];
+  const int t = threadIdx.x, d = blockIdx.x;
+  const int64_t per = (nchunks + kThreads - 1) / kThreads;
+  const int64_t c0 = (int64_t)t * per;
+  unsigned int s = 0;
+  for (int64_t c = c0; c < c0 + per && c < nchunks; ++c) s += chunk[c * 256 + d];
+  unsigned int total;
+  unsigned int run = (unsigned int)off[d] + block_excl_scan(s, s_tmp, total);
+  for (int64_t c = c0; c < c0 + per && c < nchunks; ++c) {
+    const unsigned int v = chunk[c * 256 + d];
+    chunk[c * 256 + d] = run;
+    run += v;
+  }
+}
+
+// Step 3: tile_cnt[tile][d] <- global start of digit d's run of this tile.
+__global__ __launch_bounds__(kThreads) void k_tile_bases(unsigned int* __restrict__ tile_cnt, int64_t tiles,
+                                                         const unsigned int* __restrict__ chunk) {
+  const int t = threadIdx.x;
+  const int64_t t0 = (int64_t)blockIdx.x * kScanTiles;
+  const int64_t t1 = t0 + kScanTiles < tiles ? t0 + kScanTiles : tiles;
+  unsigned int run = chunk[(int64_t)blockIdx.x * 256 + t];
+#pragma unroll 8
+  for (int64_t i = t0; i < t1; ++i) {
+    const unsigned int v = tile_cnt[i * 256 + t];
+    tile_cnt[i * 256 + t] = run;
+    run += v;
+  }
+}
+
 // Bucket start offsets (exclusive scan of each pass histogram) and the number
 // of rows that survive pass 0.
 __global__ __launch_bounds__(kThreads) void k_offsets(const unsigned long long* __restrict__ hist,
@@ -259,22 +432,25 @@ constexpr uint64_t kFlagAgg = 1ull << 46;
 constexpr uint64_t kFlagPre = 2ull << 46;
 constexpr uint64_t kFlagMask = 3ull << 46;
 constexpr uint64_t kValMask = (1ull << 46) - 1ull;
-constexpr int kLookback = 8;
+#ifndef PDP_LOOKBACK
+#define PDP_LOOKBACK 8
+#endif
+constexpr int kLookback = PDP_LOOKBACK;
 
 // LDS per block ~39 KB (half-tile record staging, digits recomputed from the
 // staged record) and <= 128 VGPRs, so 4 blocks (16 waves) share a CU: the
 // per-tile latency chain (tile claim, loads, look-back) is hidden by the
 // other blocks instead of idling the CU.
-constexpr int kHalfTile = kTile / 2;
+constexpr int kHalfTile = kTile / PDP_OS_STAGE_DIV;
 constexpr uint32_t kNoPos = 0xFFFFu;
 
 template <bool SOA>
-__global__ __launch_bounds__(kThreads, 3) void k_onesweep(
+__global__ __launch_bounds__(kThreads, PDP_OS_OCC) void k_onesweep(
     const int64_t* __restrict__ pid, const int64_t* __restrict__ pk, const double* __restrict__ val,
     const Rec* __restrict__ rin, Rec* __restrict__ rout, int64_t n_in,
     const unsigned long long* __restrict__ counters_n, int n_slot, KeySpec ks, int pass,
     const unsigned long long* __restrict__ off, unsigned long long* __restrict__ status, uint32_t epoch,
-    unsigned long long* __restrict__ counters, int tile_slot) {
+    unsigned long long* __restrict__ counters, int tile_slot, const unsigned int* __restrict__ tile_base) {
   __shared__ Rec s_rec[kHalfTile];
   __shared__ unsigned int s_cnt[4][kHist + 1];
   __shared__ unsigned int s_dstart[256];
@@ -285,10 +461,14 @@ __global__ __launch_bounds__(kThreads, 3) void k_onesweep(
 
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const long long c0 = ks.prof ? (long long)__builtin_amdgcn_s_memtime() : 0;
-  if (t == 0) s_tile = (unsigned int)atomicAdd(&counters[tile_slot], 1ull);
+  // Reduce-then-scan mode (tile_base != null): tile = block, its digit bases
+  // are precomputed; otherwise tiles are claimed in order for the look-back.
+  if (t == 0 && !tile_base) s_tile = (unsigned int)atomicAdd(&counters[tile_slot], 1ull);
   for (int i = t; i < 4 * (kHist + 1); i += kThreads) (&s_cnt[0][0])[i] = 0;
   __syncthreads();
-  const int64_t tile = s_tile;
+  const int64_t tile = tile_base ? (int64_t)blockIdx.x : (int64_t)s_tile;
+  // prefetch this tile's digit bases (their latency hides behind the loads)
+  const unsigned int tb = (tile_base && t < 256) ? tile_base[tile * 256 + t] : 0u;
   const int64_t n_eff = SOA ? n_in : (int64_t)counters_n[n_slot];
   const int64_t tile_start = tile * kTile;
   if (tile_start >= n_eff) return;
@@ -313,34 +493,92 @@ __global__ __launch_bounds__(kThreads, 3) void k_onesweep(
         else
           d = digit_of(ks, pass, r[k]);
       } else {
-        r[k] = rin[idx];
+        r[k] = ld_rec(rin + idx);
         d = digit_of(ks, pass, r[k]);
       }
     }
     dr[k] = d;
   }
 
+  long long ca = 0;
+  if (ks.prof) {
+    uint32_t dsum = 0;
+#pragma unroll
+    for (int k = 0; k < kItems; ++k) dsum += dr[k];
+    ca = (long long)__builtin_amdgcn_s_memtime() + (dsum == 0xFFFFFFFFu);  // after every load landed
+  }
   // Wave-level multisplit ranking (stable: item order = wave, k, lane).
+  // Peers = lanes with the same digit (one ballot per digit bit, plus a
+  // validity ballot when the tile can hold dropped / padding rows).  The
+  // lowest peer adds the group size to the wave's digit counter with an LDS
+  // atomic; LDS ops of one wave complete in issue order, so the returned
+  // bases are the sequential ones and the 16 atomics pipeline (no wave
+  // barriers).  The base reaches the other peers by a lane shuffle.
   const uint64_t lt = (1ull << lane) - 1ull;
+  const bool any_invalid = SOA || tile_start + kTile > n_eff;
+#if PDP_OS_RANK_ATOMIC
+  constexpr int kRankGroup = kItems < 8 ? kItems : 8;  // atomics in flight before their shuffles
+#pragma unroll
+  for (int k0 = 0; k0 < kItems; k0 += kRankGroup) {
+    uint32_t old[kRankGroup];
+#pragma unroll
+    for (int k = k0; k < k0 + kRankGroup; ++k) {
+      const uint32_t d = dr[k];
+      uint64_t peers = ~0ull;
+#pragma unroll
+      for (int b = 0; b < 8; ++b) {
+        if (b < radix_bits) {
+          const bool bit = (d >> b) & 1u;
+          const uint64_t bb = __ballot(bit);
+          peers &= bit ? bb : ~bb;
+        }
+      }
+      if (any_invalid) {
+        const bool v = d < 256;
+        const uint64_t bb = __ballot(v);
+        peers &= v ? bb : ~bb;
+      }
+      const uint32_t before = __popcll(peers & lt);
+      const uint32_t leader = (uint32_t)__ffsll((unsigned long long)peers) - 1u;
+      old[k - k0] = 0;
+      if (d < 256 && before == 0) old[k - k0] = atomicAdd(&s_cnt[wave][d], (unsigned int)__popcll(peers));
+      dr[k] = d | (before << 9) | (leader << 15);
+    }
+#pragma unroll
+    for (int k = k0; k < k0 + kRankGroup; ++k) {
+      const uint32_t basec = (uint32_t)__shfl((int)old[k - k0], (int)(dr[k] >> 15));
+      dr[k] = (dr[k] & 511u) | ((basec + ((dr[k] >> 9) & 63u)) << 9);
+    }
+  }
+  __syncthreads();
+#else
 #pragma unroll
   for (int k = 0; k < kItems; ++k) {
     const uint32_t d = dr[k];
     uint64_t peers = ~0ull;
 #pragma unroll
-    for (int b = 0; b < 9; ++b) {
-      const bool bit = (d >> b) & 1u;
-      const uint64_t bb = __ballot(bit);
-      peers &= bit ? bb : ~bb;
+    for (int b = 0; b < 8; ++b) {
+      if (b < radix_bits) {
+        const bool bit = (d >> b) & 1u;
+        const uint64_t bb = __ballot(bit);
+        peers &= bit ? bb : ~bb;
+      }
+    }
+    if (any_invalid) {  // digits 256 (dropped) / 257 (padding) share a counter
+      const bool v = d < 256;
+      const uint64_t bb = __ballot(v);
+      peers &= v ? bb : ~bb;
     }
     const uint32_t before = __popcll(peers & lt);
     const uint32_t c = __popcll(peers);
     const uint32_t basec = s_cnt[wave][d];
     __builtin_amdgcn_wave_barrier();
-    if (before == 0) s_cnt[wave][d] = basec + c;
+    if (before == 0 && d < 256) s_cnt[wave][d] = basec + c;
     __builtin_amdgcn_wave_barrier();
     dr[k] = d | ((basec + before) << 9);
   }
   __syncthreads();
+#endif
 
   // Per-digit tile counts, per-wave exclusive offsets, digit starts.
   unsigned int tcount = 0;
@@ -360,7 +598,11 @@ __global__ __launch_bounds__(kThreads, 3) void k_onesweep(
 
   const long long c1 = ks.prof ? (long long)__builtin_amdgcn_s_memtime() : 0;
   // Decoupled look-back per digit.
-  if (t < radix) {
+  if (tile_base) {
+    if (t < radix) s_gbase[t] = (long long)tb - (long long)dstart;
+  } else if (t < radix && (ks.ablate & kDebugNoLookback)) {
+    s_gbase[t] = (long long)off[t] - (long long)dstart;
+  } else if (t < radix) {
     unsigned long long* st = status + (size_t)tile * kStatusStride;
     const uint64_t ep = (uint64_t)epoch << 48;
     uint64_t excl = 0;
@@ -428,15 +670,19 @@ __global__ __launch_bounds__(kThreads, 3) void k_onesweep(
     const unsigned int e = tot - h < (unsigned int)kHalfTile ? tot - h : (unsigned int)kHalfTile;
     for (unsigned int i = t; i < e; i += kThreads) {
       const Rec rc = s_rec[i];
-      rout[s_gbase[digit_of(ks, pass, rc)] + (long long)(h + i)] = rc;
+      if (ks.ablate & kDebugLinearWrite)
+        st_rec(rout + tile_start + (long long)(h + i), rc);
+      else
+        st_rec(rout + s_gbase[digit_of(ks, pass, rc)] + (long long)(h + i), rc);
     }
     __syncthreads();
   }
   if (ks.prof && t == 0) {
     const long long c3 = (long long)__builtin_amdgcn_s_memtime();
-    atomicAdd(&counters[kCtrSweepCycles], (unsigned long long)(c1 - c0));
-    atomicAdd(&counters[kCtrSweepCycles + 1], (unsigned long long)(c2 - c1));
-    atomicAdd(&counters[kCtrSweepCycles + 2], (unsigned long long)(c3 - c2));
+    atomicAdd(&counters[kCtrSweepCycles], (unsigned long long)(ca - c0));
+    atomicAdd(&counters[kCtrSweepCycles + 1], (unsigned long long)(c1 - ca));
+    atomicAdd(&counters[kCtrSweepCycles + 2], (unsigned long long)(c2 - c1));
+    atomicAdd(&counters[kCtrSweepCycles + 3], (unsigned long long)(c3 - c2));
     atomicAdd(&counters[kCtrSweepTiles], 1ull);
   }
   (void)radix_bits;
@@ -472,6 +718,7 @@ __device__ __forceinline__ void row_terms(const SegParams& sp, double v, double&
 
 __device__ __forceinline__ void emit_group(const SegParams& sp, const AccPtrs& acc, uint32_t pk, uint32_t cnt,
                                            double x, double y) {
+  if (sp.debug & kDebugNoAtomics) return;
   if (sp.packed) {
     // one 64-bit atomic for (count, row_count); both stay < 2^32 (rows < 2^32)
     atomicAdd(&acc.row_count[pk], ((unsigned long long)cnt << 32) | 1ull);
@@ -973,6 +1220,36 @@ int scan_inplace(long long* a, int64_t n, hipStream_t stream) {
   return 0;
 }
 
+// Reduce-then-scan radix passes: tile digit counts (written by K0 for pass 0,
+// by k_tile_counts otherwise) -> per-tile global digit bases in place.
+// `tile_cnt` and the chunk sums live in the look-back status region (so the
+// next look-back use re-zeroes it).  Needs rows < 2^32 (u32 bases).
+struct TileScan {
+  unsigned int* tile_cnt;
+  unsigned int* chunk;
+  int64_t tiles;
+};
+
+TileScan tile_scan_bufs(pdp_ctx* ctx, unsigned long long* status, int64_t tiles) {
+  ctx->last_ws = nullptr;
+  TileScan ts;
+  ts.tile_cnt = (unsigned int*)status;
+  ts.chunk = ts.tile_cnt + (size_t)tiles * 256;
+  ts.tiles = tiles;
+  return ts;
+}
+
+bool use_tile_scan(int64_t n, int debug) { return n < (1ll << 32) && !(debug & kDebugLookback); }
+
+void tile_scan(const TileScan& ts, const unsigned long long* off_pass, hipStream_t stream) {
+  const int64_t nchunks = (ts.tiles + kScanTiles - 1) / kScanTiles;
+  hipLaunchKernelGGL(k_tile_chunk_sums, dim3((unsigned)nchunks), dim3(kThreads), 0, stream, ts.tile_cnt, ts.tiles,
+                     ts.chunk);
+  hipLaunchKernelGGL(k_tile_chunk_scan, dim3(256), dim3(kThreads), 0, stream, ts.chunk, nchunks, off_pass);
+  hipLaunchKernelGGL(k_tile_bases, dim3((unsigned)nchunks), dim3(kThreads), 0, stream, ts.tile_cnt, ts.tiles,
+                     ts.chunk);
+}
+
 // LSD sort of `m` records (a <-> b ping-pong) by the passes of `ks`; the
 // sorted array pointer is returned in *out.
 int sort_recs(pdp_ctx* ctx, Rec* a, Rec* b, int64_t m, const KeySpec& ks, unsigned long long* hist,
@@ -996,13 +1273,23 @@ int sort_recs(pdp_ctx* ctx, Rec* a, Rec* b, int64_t m, const KeySpec& ks, unsign
   Rec* src = a;
   Rec* dst = b;
   const int64_t tiles = (m + kTile - 1) / kTile;
+  const bool rts = use_tile_scan(m, 0);
   for (int p = 0; p < ks.passes; ++p) {
-    int rc = next_epoch(ctx, stream, status, status_bytes, ws);
-    if (rc) return rc;
+    const unsigned int* bases = nullptr;
+    if (rts) {
+      const TileScan ts = tile_scan_bufs(ctx, status, tiles);
+      hipLaunchKernelGGL(k_tile_counts, dim3(grid_for(tiles, 1, 4096)), dim3(kThreads), 0, stream, src, counters,
+                         (int)kCtrNGeneric, ks, p, tiles, ts.tile_cnt);
+      tile_scan(ts, off + p * kHist, stream);
+      bases = ts.tile_cnt;
+    } else {
+      int rc = next_epoch(ctx, stream, status, status_bytes, ws);
+      if (rc) return rc;
+    }
     hipLaunchKernelGGL(k_onesweep<false>, dim3((unsigned)tiles), dim3(kThreads), 0, stream,
                        (const int64_t*)nullptr, (const int64_t*)nullptr, (const double*)nullptr, src, dst, m,
                        counters, (int)kCtrNGeneric, ks, p, off + p * kHist, status, ctx->epoch, counters,
-                       (int)ctx->tile_slot++);
+                       (int)ctx->tile_slot++, bases);
     std::swap(src, dst);
   }
   HIP_TRY(hipGetLastError());
@@ -1368,34 +1655,55 @@ int pdp_bound_accumulate(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_
   }
   ctx->stats.sort_passes = plan.passes;
   ks.prof = (sp.debug & kDebugSweepStamps) != 0;
+  ks.ablate = (sp.debug & kDebugSortOnly) ? (sp.debug & (kDebugNoLookback | kDebugLinearWrite)) : 0;
+  const bool rts = use_tile_scan(n, sp.debug);
+  const TileScan ts = rts ? tile_scan_bufs(ctx, status, L.tiles) : TileScan{};
   {
     ProfScope ps(ctx, PDP_STAGE_HISTOGRAM, stream);
-    hipLaunchKernelGGL(k_histogram<true>, dim3(grid_for(n, kThreads, 2048)), dim3(kThreads), 0, stream, cols->pid,
-                       cols->pk, (const Rec*)nullptr, n, ks, hist, counters);
+    if (rts)
+      hipLaunchKernelGGL(k_histogram_tiles, dim3(grid_for(L.tiles, 1, 4096)), dim3(kThreads), 0, stream, cols->pid,
+                         cols->pk, n, ks, hist, ts.tile_cnt, counters);
+    else
+      hipLaunchKernelGGL(k_histogram<true>, dim3(grid_for(n, kThreads, 2048)), dim3(kThreads), 0, stream,
+                         cols->pid, cols->pk, (const Rec*)nullptr, n, ks, hist, counters);
   }
   hipLaunchKernelGGL(k_offsets, dim3(1), dim3(kThreads), 0, stream, hist, off, ks.passes, n, counters,
                      (int)kCtrNKept);
   Rec* src = nullptr;
   Rec* dst = recs_a;
   for (int p = 0; p < ks.passes; ++p) {
-    int rc = next_epoch(ctx, stream, status, status_bytes, workspace);
-    if (rc) return rc;
+    const unsigned int* bases = nullptr;
+    if (rts) {
+      ProfScope ps(ctx, PDP_STAGE_TILE_COUNTS, stream);
+      if (p > 0)
+        hipLaunchKernelGGL(k_tile_counts, dim3(grid_for(L.tiles, 1, 4096)), dim3(kThreads), 0, stream, src, counters,
+                           (int)kCtrNKept, ks, p, L.tiles, ts.tile_cnt);
+      tile_scan(ts, off + p * kHist, stream);
+      bases = ts.tile_cnt;
+    } else {
+      int rc = next_epoch(ctx, stream, status, status_bytes, workspace);
+      if (rc) return rc;
+    }
     ProfScope ps(ctx, p == 0 ? PDP_STAGE_ONESWEEP_FIRST : PDP_STAGE_ONESWEEP_REST, stream);
     if (p == 0)
       hipLaunchKernelGGL(k_onesweep<true>, dim3((unsigned)L.tiles), dim3(kThreads), 0, stream, cols->pid, cols->pk,
                          cols->value, (const Rec*)nullptr, dst, n, counters, (int)kCtrNKept, ks, p, off + p * kHist,
-                         status, ctx->epoch, counters, (int)ctx->tile_slot++);
+                         status, ctx->epoch, counters, (int)ctx->tile_slot++, bases);
     else
       hipLaunchKernelGGL(k_onesweep<false>, dim3((unsigned)L.tiles), dim3(kThreads), 0, stream,
                          (const int64_t*)nullptr, (const int64_t*)nullptr, (const double*)nullptr, src, dst, n,
                          counters, (int)kCtrNKept, ks, p, off + p * kHist, status, ctx->epoch, counters,
-                         (int)ctx->tile_slot++);
+                         (int)ctx->tile_slot++, bases);
     src = dst;
     dst = (dst == recs_a) ? recs_b : recs_a;
   }
   HIP_TRY(hipGetLastError());
   Rec* sorted = src;
   Rec* spare = dst;
+  if (sp.debug & kDebugSortOnly) {
+    HIP_TRY(hipStreamSynchronize(stream));
+    return 0;
+  }
 
   OvList ov{ranges, counters};
   BigList big{(unsigned long long*)(ws + L.big), L.big_cap};
@@ -1414,11 +1722,11 @@ int pdp_bound_accumulate(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_
   }
   HIP_TRY(hipGetLastError());
 
-  unsigned long long host_ctr[12];
+  unsigned long long host_ctr[13];
   HIP_TRY(hipMemcpyAsync(host_ctr, counters, sizeof(host_ctr), hipMemcpyDeviceToHost, stream));
   HIP_TRY(hipStreamSynchronize(stream));
   ctx->stats.kept_rows_in = (int64_t)host_ctr[kCtrNKept];
-  for (int i = 0; i < 3; ++i) ctx->stats.sweep_cycles[i] = (int64_t)host_ctr[kCtrSweepCycles + i];
+  for (int i = 0; i < 4; ++i) ctx->stats.sweep_cycles[i] = (int64_t)host_ctr[kCtrSweepCycles + i];
   ctx->stats.sweep_tiles = (int64_t)host_ctr[kCtrSweepTiles];
   if (host_ctr[kCtrErr]) return fail(PDP_ERR_INTERNAL, "radix look-back timed out");
   if (host_ctr[kCtrInvalid]) return fail(PDP_ERR_OUT_OF_RANGE, "privacy id or partition id out of range");

@@ -56,7 +56,7 @@ class Outputs(ctypes.Structure):
 
 class Stats(ctypes.Structure):
     _fields_ = [("kept_rows_in", c_i64), ("fallback_rows", c_i64), ("fallback_ranges", c_i64),
-                ("sort_passes", c_i32), ("bucket_low_bits", c_i32), ("sweep_cycles", c_i64 * 3),
+                ("sort_passes", c_i32), ("bucket_low_bits", c_i32), ("sweep_cycles", c_i64 * 4),
                 ("sweep_tiles", c_i64)]
 
 
@@ -85,7 +85,8 @@ SIGNATURES = [
     ("pdp_profile_read", c_i32, [c_vp, ctypes.POINTER(c_f64), ctypes.POINTER(c_i64), c_i32]),
 ]
 
-STAGES = ["histogram", "onesweep_first", "onesweep_rest", "buckets", "generic", "release", "enforced"]
+STAGES = ["histogram", "onesweep_first", "onesweep_rest", "buckets", "generic", "release", "enforced",
+          "tile_counts"]
 
 _lib = None
 
