@@ -92,9 +92,10 @@ class World:
         keep_all = keep.new_empty(padded)
         dist.all_gather_into_tensor(keep_all, keep.contiguous()[:b], group=self.group)
         f = out.shape[0]
-        out_all = out.new_empty((self.size, f, b))
-        dist.all_gather_into_tensor(out_all, out.contiguous(), group=self.group)
-        out_all = out_all.permute(1, 0, 2).reshape(f, padded)
+        # concatenated along dim 0 ((size*F, B): the layout every backend accepts)
+        out_all = out.new_empty((self.size * f, b))
+        dist.all_gather_into_tensor(out_all, out[:, :b].contiguous(), group=self.group)
+        out_all = out_all.reshape(self.size, f, b).permute(1, 0, 2).reshape(f, padded)
         return keep_all[:num_partitions], out_all[:, :num_partitions], fields
 
 
