@@ -19,7 +19,8 @@ import shutil
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-STAGE_OF = {"k_histogram": "histogram", "k_segments": "buckets", "k_release": "release"}
+STAGE_OF = {"k_histogram": "histogram", "k_segments": "buckets", "k_lean": "buckets", "k_release": "release",
+            "k_histogram_tiles": "histogram", "k_tile_counts": "tile_counts"}
 
 
 def dispatches(path, counter):
@@ -30,7 +31,7 @@ def dispatches(path, counter):
 
 def last_step(rows):
     """Dispatches of the last pipeline step (from the last k_histogram on)."""
-    starts = [i for i, r in enumerate(rows) if r["Kernel_Name"] == "k_histogram"]
+    starts = [i for i, r in enumerate(rows) if r["Kernel_Name"] in ("k_histogram", "k_histogram_tiles")]
     out = rows[starts[-1]:]
     end = next((i for i, r in enumerate(out) if r["Kernel_Name"] == "k_release"), len(out) - 1)
     return out[:end + 1]
