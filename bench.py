@@ -21,24 +21,43 @@ sys.path.insert(0, ROOT)
 
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 
+# Per-GPU shapes of BASELINE.json configs (SURVEY.md 8(d) "Synthetic inputs").
+# c3 is the headline: COUNT+SUM+MEAN, private selection, 1e9 rows / 1e6 Zipf partitions.
+# c2: COUNT+SUM over 1e5 PUBLIC partitions (no selection), 1e8 rows, 1e6 uniform pids.
+# c4: high-cardinality stress, one GPU's shard of 4e9 rows / 5e7 Zipf partitions, L0=32.
+WORKLOADS = {
+    "c3": dict(rows=1e9, partitions=1e6, pids=1e7, zipf=1.1, l0=4, linf=2, public=False, metrics="mean",
+               cpu_sample=12e6),
+    "c2": dict(rows=1e8, partitions=1e5, pids=1e6, zipf=0.0, l0=8, linf=4, public=True, metrics="count_sum",
+               cpu_sample=12e6),
+    "c4": dict(rows=5e8, partitions=5e7, pids=1.25e7, zipf=1.1, l0=32, linf=4, public=False, metrics="mean",
+               cpu_sample=5e5),  # the oracle's O(P) release dominates at P=5e7
+}
+
 
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=2)
-    p.add_argument("--rows", type=float, default=1e9, help="rows per GPU")
-    p.add_argument("--partitions", type=float, default=1e6)
-    p.add_argument("--pids", type=float, default=1e7, help="privacy ids per GPU")
-    p.add_argument("--zipf", type=float, default=1.1)
-    p.add_argument("--l0", type=int, default=4)
-    p.add_argument("--linf", type=int, default=2)
-    p.add_argument("--cpu-sample", type=float, default=12e6, help="rows of the CPU baseline sample")
+    p.add_argument("--workload", choices=sorted(WORKLOADS), default="c3",
+                   help="c3 = headline (BASELINE.json metric); c2 / c4 = the other single-GPU-sized configs")
+    p.add_argument("--rows", type=float, default=None, help="rows per GPU")
+    p.add_argument("--partitions", type=float, default=None)
+    p.add_argument("--pids", type=float, default=None, help="privacy ids per GPU")
+    p.add_argument("--zipf", type=float, default=None)
+    p.add_argument("--l0", type=int, default=None)
+    p.add_argument("--linf", type=int, default=None)
+    p.add_argument("--cpu-sample", type=float, default=None, help="rows of the CPU baseline sample")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-profile", action="store_true")
     p.add_argument("--seed", type=int, default=20250204)
     p.add_argument("--debug-flags", type=int, default=0, help="kernel ablation flags (experiments only)")
-    return p.parse_args()
+    args = p.parse_args()
+    for k, v in WORKLOADS[args.workload].items():
+        if getattr(args, k, None) is None:
+            setattr(args, k, v)
+    return args
 
 
 def stage_bytes(stage, n_in, n_kept, P, nfields):
@@ -79,14 +98,17 @@ def cpu_baseline(args, P):
     U = max(1, int(args.pids * m / args.rows))
     pid, pk, val = o.synth_rows(m, U, P, seed=args.seed, zipf_s=args.zipf)
     bp = o.BoundParams(args.l0, args.linf, 0.0, 10.0)
-    spec = o.ReleaseSpec(("mean", "count", "sum"), "laplace", {"mean": (0.5, 0.0)}, "truncated_geometric",
-                         (0.5, 1e-6))
+    if WORKLOADS[args.workload]["public"]:
+        spec = o.ReleaseSpec(("count", "sum"), "laplace", {"count": (0.5, 0.0), "sum": (0.5, 0.0)}, None)
+    else:
+        spec = o.ReleaseSpec(("mean", "count", "sum"), "laplace", {"mean": (0.5, 0.0)}, "truncated_geometric",
+                             (0.5, 1e-6))
     t0 = time.perf_counter()
     acc = o.bound_and_accumulate(pid, pk, val, P, bp, "hash", seed=1)
     o.release(acc, bp, spec, seed=2)
     dt = time.perf_counter() - t0
     return {"value": m / dt, "unit": "rows/s", "cores": 1, "kind": "port",
-            "sample": f"{m} rows, {U} privacy ids, {P} Zipf({args.zipf}) partitions; numpy oracle "
+            "sample": f"{args.workload}: {m} rows, {U} privacy ids, {P} Zipf({args.zipf}) partitions; numpy oracle "
                       f"(oracle/pdp_oracle.py) on 1 host core, {dt:.1f} s"}
 
 
@@ -113,16 +135,22 @@ def main():
     U = int(args.pids)
     ex = HipExecutor(local)
     pid, pk, val = ex.generate(n, U, P, seed=args.seed, zipf_s=args.zipf, lo=0.0, hi=10.0, row_offset=rank * n)
-    mask = native.METRIC_COUNT | native.METRIC_SUM | native.METRIC_MEAN
+    public = WORKLOADS[args.workload]["public"]
+    count_sum = WORKLOADS[args.workload]["metrics"] == "count_sum"
+    mask = native.METRIC_COUNT | native.METRIC_SUM | (0 if count_sum else native.METRIC_MEAN)
     bounds = BoundConfig(mask, args.l0, args.linf, 0.0, 10.0, sampling_seed=args.seed + 1,
                          debug_flags=args.debug_flags)
     # NaiveBudgetAccountant(eps=1, delta=1e-6): MeanCombiner (Laplace) eps 0.5, selection eps 0.5 delta 1e-6
     eps = [0.0] * 6
     delta = [0.0] * 6
-    eps[native.MECH_MEAN] = 0.5
-    eps[native.MECH_SELECTION], delta[native.MECH_SELECTION] = 0.5, 1e-6
-    rel = ReleaseConfig(mask, native.NOISE_LAPLACE, native.SELECTION_TRUNCATED_GEOMETRIC, eps, delta, 1, True,
-                        noise_seed=args.seed + 2)
+    if count_sum:  # public partitions: the whole budget goes to COUNT and SUM (weights 1:1)
+        eps[native.MECH_COUNT] = eps[native.MECH_SUM] = 0.5
+    else:
+        eps[native.MECH_MEAN] = 0.5
+    if not public:
+        eps[native.MECH_SELECTION], delta[native.MECH_SELECTION] = 0.5, 1e-6
+    selection = native.SELECTION_NONE if public else native.SELECTION_TRUNCATED_GEOMETRIC
+    rel = ReleaseConfig(mask, native.NOISE_LAPLACE, selection, eps, delta, 1, True, noise_seed=args.seed + 2)
     fields = native.metric_fields(mask)
 
     def step():
@@ -195,9 +223,12 @@ def main():
             "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f64",
             "data": "synthetic (on-device Philox generator, oracle/pdp_oracle.py:synth_rows)",
-            "config": {"workload": f"DP COUNT+SUM+MEAN, {n:.2e} rows/GPU, {U:.1e} privacy ids/GPU, "
-                                   f"{P:.1e} Zipf({args.zipf}) partitions, L0={args.l0}, Linf={args.linf}, "
-                                   f"[0,10], Laplace, truncated-geometric selection, eps=1 delta=1e-6",
+            "config": {"workload": f"{args.workload}: DP {'COUNT+SUM' if count_sum else 'COUNT+SUM+MEAN'}, "
+                                   f"{n:.2e} rows/GPU, {U:.1e} privacy ids/GPU, {P:.1e} "
+                                   f"{'public uniform' if public else f'Zipf({args.zipf})'} partitions, "
+                                   f"L0={args.l0}, Linf={args.linf}, [0,10], Laplace, "
+                                   f"{'no selection (public partitions)' if public else 'truncated-geometric selection'}"
+                                   f", eps=1 delta=1e-6",
                        "rows_per_gpu": n, "partitions": P, "privacy_ids_per_gpu": U,
                        "parallelism": f"pid-sharded x{world_size}" + (" + RCCL reduce-scatter" if world else "")},
             "roofline": roofline, "cpu_baseline": cpu,

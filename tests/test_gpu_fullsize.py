@@ -1,0 +1,88 @@
+"""GPU parity at BASELINE.json's full sizes, through size-independent properties.
+
+The CPU oracle cannot run 1e9 rows in test time, so at full size the HIP path
+(through the C ABI) is checked against invariants computed independently with
+plain torch ops on the same device-resident inputs:
+
+* non-binding bounds (every pid has <= L0 partitions and every pair <= Linf rows,
+  asserted on the data): count == bincount(pk) and privacy-id count == distinct
+  pids per pk, bit-exact; sum == index_add of the values, |d| <= 1e-9 * (sum of
+  |terms| + 1) (fp64, summation order differs) -- the reference's
+  `combine_accumulators_per_key` (`pipeline_backend.py:528-538`) with nothing
+  sampled away;
+* binding bounds (the headline config, c3 shape): each pid keeps exactly
+  min(#partitions, L0) partitions (`contribution_bounders.py:90-92`), so
+  sum(privacy-id count) == sum_pid min(npk, L0) bit-exact; per pk
+  row_count <= count <= min(Linf * row_count, rows of pk)
+  (`contribution_bounders.py:74-76`); |sum(clip - mid)| <= count * (b - a) / 2;
+* determinism: a second run with the same seed gives identical counts.
+"""
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+MASK_COUNT, MASK_SUM, MASK_MEAN, MASK_PID = 1, 2, 4, 16
+
+
+@pytest.fixture(scope="module")
+def ex():
+    from pipelinedp_amd.executor import HipExecutor
+    return HipExecutor(0)
+
+
+def _pairs(torch, pid, pk, P):
+    """Distinct (pid, pk) pairs as sorted int64 keys pid*P + pk."""
+    return torch.unique(pid * P + pk, sorted=True)
+
+
+def test_non_binding_200m_rows_exact(ex):
+    import torch
+    from pipelinedp_amd.executor import BoundConfig
+    n, U, P, L0, Linf = 200_000_000, 100_000_000, 100_000, 16, 16
+    pid, pk, val = ex.generate(n, U, P, seed=0x5EED0002, zipf_s=0.0, lo=0.0, hi=10.0)
+    keys = _pairs(torch, pid, pk, P)
+    per_pid = torch.bincount(keys // P, minlength=U)
+    assert int(per_pid.max()) <= L0
+    _, mult = torch.unique_consecutive(torch.sort(pid * P + pk).values, return_counts=True)
+    assert int(mult.max()) <= Linf
+    del mult
+
+    cfg = BoundConfig(MASK_COUNT | MASK_SUM | MASK_PID, L0, Linf, 0.0, 10.0, sampling_seed=9)
+    acc = ex.accumulate(pid, pk, val, U, P, cfg)
+    torch.cuda.synchronize()
+    assert torch.equal(acc.count, torch.bincount(pk, minlength=P))
+    assert torch.equal(acc.row_count, torch.bincount(keys % P, minlength=P))
+    ref = torch.zeros(P, dtype=torch.float64, device=pid.device).index_add_(0, pk, val)
+    absref = torch.zeros_like(ref).index_add_(0, pk, val.abs())
+    assert bool(((acc.x - ref).abs() <= 1e-9 * (absref + 1.0)).all())
+
+
+def test_headline_1b_rows_binding_invariants(ex):
+    import torch
+    from pipelinedp_amd.executor import BoundConfig
+    n, U, P, L0, Linf, a, b = 1_000_000_000, 10_000_000, 1_000_000, 4, 2, 0.0, 10.0
+    pid, pk, val = ex.generate(n, U, P, seed=20250204, zipf_s=1.1, lo=a, hi=b)
+    mask = MASK_COUNT | MASK_SUM | MASK_MEAN | MASK_PID
+    cfg = BoundConfig(mask, L0, Linf, a, b, sampling_seed=13)
+    acc = ex.accumulate(pid, pk, val, U, P, cfg)
+    torch.cuda.synchronize()
+    rc, cnt, nsum = acc.row_count.clone(), acc.count.clone(), acc.x.clone()
+
+    rows_pk = torch.bincount(pk, minlength=P)
+    keys = _pairs(torch, pid, pk, P)
+    del pid, val
+    npk = torch.bincount(keys // P, minlength=U)
+    assert int(rc.sum()) == int(npk.clamp(max=L0).sum())
+    assert bool((rc <= torch.bincount(keys % P, minlength=P)).all())
+    del keys, npk
+    assert bool((cnt >= rc).all())
+    assert bool((cnt <= torch.minimum(Linf * rc, rows_pk)).all())
+    assert bool((nsum.abs() <= cnt.to(torch.float64) * (b - a) / 2 + 1e-6).all())
+
+    pid, pk, val = ex.generate(n, U, P, seed=20250204, zipf_s=1.1, lo=a, hi=b)
+    acc2 = ex.accumulate(pid, pk, val, U, P, cfg)
+    torch.cuda.synchronize()
+    assert torch.equal(acc2.row_count, rc)
+    assert torch.equal(acc2.count, cnt)
+    absmax = cnt.to(torch.float64) * (b - a) / 2
+    assert bool(((acc2.x - nsum).abs() <= 1e-9 * (absmax + 1.0)).all())
