@@ -149,6 +149,7 @@ constexpr int kDebugNoLookback = 32768;
 constexpr int kDebugLinearWrite = 65536;
 constexpr int kDebugLookback = 131072;  // radix passes by decoupled look-back instead of reduce-then-scan
 constexpr int kDebugNoAtomics = 262144;  // K2 skips its accumulator atomics (timing ablation)
+constexpr int kDebugNoHotCache = 524288;  // k_lean emits straight to HBM (no LDS partition cache)
 
 struct AccPtrs {
   unsigned long long* row_count;
@@ -1712,7 +1713,8 @@ int pdp_bound_accumulate(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_
     ProfScope ps(ctx, PDP_STAGE_BUCKETS, stream);
     if (bp->max_partitions_contributed <= kLeanMaxL0 && !(sp.debug & kDebugBatchKernel)) {
       const int64_t waves = (n + kLeanChunk - 1) / kLeanChunk;
-      hipLaunchKernelGGL(k_lean, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, stream, sorted, counters,
+      const int64_t blocks = (waves + 3) / 4 < kLeanMaxBlocks ? (waves + 3) / 4 : kLeanMaxBlocks;
+      hipLaunchKernelGGL(k_lean, dim3((unsigned)blocks), dim3(256), 0, stream, sorted, counters,
                          (int)kCtrNKept, sp, acc, ov, big, (int)bp->debug_force_fallback);
     } else {
       hipLaunchKernelGGL(k_segments, dim3((unsigned)seg_grid), dim3(kThreads), 0, stream, sorted, counters,

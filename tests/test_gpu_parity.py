@@ -69,6 +69,9 @@ CONFIGS = [
     (60000, 400, 5000, 1.1, 4, 2, (0.0, 10.0), None, 1 | 2 | 4),  # ~150 rows / pid: lean + big-batch kernels
     (40000, 2000, 300, 1.3, 16, 1, (0.0, 5.0), None, 1 | 4 | 8 | 16),  # largest L0 of the lean kernel
     (30000, 1000, 3, 0.0, 2, 8, (0.0, 10.0), None, 1 | 2),  # groups of > 4 kept rows (wave-sum path)
+    (40000, 500, 3000, 1.1, 32, 2, (0.0, 10.0), None, 1 | 2 | 4 | 16),  # c4-like L0=32, binding for some pids
+    (30000, 250, 20000, 0.0, 64, 3, (-1.0, 9.0), None, 1 | 4 | 8 | 16),  # L0=64: every lane holds a kept group
+    (30000, 250, 20000, 0.0, 65, 3, (0.0, 10.0), None, 1 | 2),  # L0 > 64: batch kernel
 ]
 
 
