@@ -168,6 +168,20 @@ int pdp_bound_accumulate(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_
                          const pdp_accumulators* acc, void* workspace, size_t workspace_bytes,
                          void* stream);
 
+/* Bounding sweep (utility analysis over many bounding configurations, the
+ * per-configuration DPEngine runs of analysis/utility_analysis_engine.py:
+ * 88-173 with MultiParameterConfiguration, analysis/data_structures.py):
+ * rows are sorted by privacy id ONCE, then bounded and accumulated per
+ * configuration into accs[c].  bps[c] may differ in L0, L_inf, value / sum
+ * bounds, metrics and sampling seed; accs[c] follows pdp_bound_accumulate.
+ * Result c equals pdp_bound_accumulate(cols, &bps[c], &accs[c]).
+ * contribution_bounds_already_enforced is rejected.  Workspace:
+ * pdp_sweep_workspace_size (one more record buffer than a single run). */
+int pdp_sweep_workspace_size(const pdp_columns* cols, size_t* bytes);
+int pdp_bound_accumulate_sweep(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bps,
+                               int32_t num_configs, const pdp_accumulators* accs, void* workspace,
+                               size_t workspace_bytes, void* stream);
+
 /* Accumulators of partitions [pk_offset, pk_offset + num_partitions) ->
  * selection + noisy metrics.  Philox counters use the global partition id
  * (pk_offset + i), so the result does not depend on how partitions are

@@ -1063,17 +1063,18 @@ int grid_for(int64_t n, int threads, int cap = 4096) {
 }
 
 struct Layout {
-  size_t recs_a, recs_b, hist, off, counters, status, ranges, big, total;
+  size_t recs_a, recs_b, recs_c, hist, off, counters, status, ranges, big, total;
   int64_t tiles;
   uint64_t big_cap;
 };
 
-Layout layout_for(int64_t n) {
+Layout layout_for(int64_t n, bool sweep = false) {
   Layout L{};
   size_t o = 0;
   const size_t rb = align_up((size_t)std::max<int64_t>(n, 1) * sizeof(Rec), 256);
   L.recs_a = o; o += rb;
   L.recs_b = o; o += rb;
+  L.recs_c = o; o += sweep ? rb : 0;  // sweep: generic-path scratch that keeps the sorted rows intact
   L.hist = o; o += align_up(kMaxPasses * kHist * 8, 256);
   L.off = o; o += align_up(kMaxPasses * kHist * 8, 256);
   L.counters = o; o += align_up(kNumCounters * 8, 256);
@@ -1325,7 +1326,10 @@ KeySpec composite_spec(int mode, int hi_bits, int lo_bits, int pkb, uint32_t U, 
   return ks;
 }
 
-int run_generic(pdp_ctx* ctx, Rec* sorted, Rec* spare, const std::vector<unsigned long long>& ranges,
+// `sorted` is only read (gather); `alt` is the generic sort's second buffer
+// (== sorted on the single-config path, a third buffer in a sweep so the
+// sorted rows survive for the next configuration).
+int run_generic(pdp_ctx* ctx, const Rec* sorted, Rec* spare, Rec* alt, const std::vector<unsigned long long>& ranges,
                 const Plan& plan, const SegParams& sp, const pdp_bound_params* bp, uint32_t U, uint32_t P,
                 AccPtrs acc, unsigned long long* hist, unsigned long long* off, unsigned long long* counters,
                 unsigned long long* status, size_t status_bytes, void* ws, hipStream_t stream) {
@@ -1353,10 +1357,10 @@ int run_generic(pdp_ctx* ctx, Rec* sorted, Rec* spare, const std::vector<unsigne
 
   // 1) rows by (pid, pk), stable (input order within a group)
   Rec* r = nullptr;
-  int rc = sort_recs(ctx, spare, sorted, total, composite_spec(1, plan.pidb, plan.pkb, plan.pkb, U, P), hist, off,
+  int rc = sort_recs(ctx, spare, alt, total, composite_spec(1, plan.pidb, plan.pkb, plan.pkb, U, P), hist, off,
                      counters, status, status_bytes, ws, stream, &r);
   if (rc) return rc;
-  Rec* r_other = (r == spare) ? sorted : spare;
+  Rec* r_other = (r == spare) ? alt : spare;
 
   const size_t m8 = (size_t)total * 8;
   long long *gsc, *psc, *gpos, *pfirst;
@@ -1572,44 +1576,71 @@ int pdp_workspace_size(const pdp_columns* cols, const pdp_bound_params* bp, size
   return 0;
 }
 
+int pdp_sweep_workspace_size(const pdp_columns* cols, size_t* bytes) {
+  if (!cols || !bytes) return fail(PDP_ERR_INVALID_ARG, "null argument");
+  if (cols->num_rows < 0) return fail(PDP_ERR_INVALID_ARG, "num_rows < 0");
+  *bytes = layout_for(cols->num_rows, true).total;
+  return 0;
+}
+
 int pdp_get_stats(pdp_ctx* ctx, pdp_stats* out) {
   if (!ctx || !out) return fail(PDP_ERR_INVALID_ARG, "null argument");
   *out = ctx->stats;
   return 0;
 }
 
-int pdp_bound_accumulate(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp,
-                         const pdp_accumulators* accp, void* workspace, size_t workspace_bytes, void* stream_) {
-  if (!ctx || !cols || !bp || !accp) return fail(PDP_ERR_INVALID_ARG, "null argument");
+namespace {
+
+// pdp_bound_accumulate (nconf == 1, sweep == false) and
+// pdp_bound_accumulate_sweep: K0/K1 sort the rows by privacy id ONCE (the
+// order does not depend on L0 / L_inf / clipping), then K2 (+ KF) runs per
+// configuration over the same sorted rows.
+int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bps, int nconf,
+               const pdp_accumulators* accps, void* workspace, size_t workspace_bytes, void* stream_, bool sweep) {
+  if (!ctx || !cols || !bps || !accps) return fail(PDP_ERR_INVALID_ARG, "null argument");
+  if (nconf < 1) return fail(PDP_ERR_INVALID_ARG, "num_configs must be >= 1");
   hipStream_t stream = (hipStream_t)stream_;
+  const pdp_bound_params* bp = &bps[0];
   const int64_t n = cols->num_rows, U = cols->num_privacy_ids, P = cols->num_partitions;
   if (n < 0 || P < 1 || P > (1ll << 31)) return fail(PDP_ERR_INVALID_ARG, "num_partitions must be in [1, 2^31]");
   if (!bp->bounds_already_enforced && (U < 1 || U > (1ll << 32)))
     return fail(PDP_ERR_INVALID_ARG, "num_privacy_ids must be in [1, 2^32]");
-  if (bp->max_partitions_contributed < 1 || bp->max_contributions_per_partition < 1)
-    return fail(PDP_ERR_INVALID_ARG, "contribution bounds must be positive");
-  const int m = bp->metrics;
-  const bool need_value = (m & (PDP_METRIC_SUM | PDP_METRIC_MEAN | PDP_METRIC_VARIANCE)) != 0;
-  if (need_value && n > 0 && !cols->value) return fail(PDP_ERR_INVALID_ARG, "value column required for SUM/MEAN/VARIANCE");
+  const Plan plan = make_plan(n, std::max<int64_t>(U, 1), P);
+  std::vector<SegParams> sps(nconf);
+  std::vector<AccPtrs> accs(nconf);
+  for (int c = 0; c < nconf; ++c) {
+    const pdp_bound_params* b = &bps[c];
+    const pdp_accumulators* a = &accps[c];
+    if (sweep && b->bounds_already_enforced)
+      return fail(PDP_ERR_INVALID_ARG, "a sweep cannot use contribution_bounds_already_enforced");
+    if (b->max_partitions_contributed < 1 || b->max_contributions_per_partition < 1)
+      return fail(PDP_ERR_INVALID_ARG, "contribution bounds must be positive");
+    const bool need_value = (b->metrics & (PDP_METRIC_SUM | PDP_METRIC_MEAN | PDP_METRIC_VARIANCE)) != 0;
+    if (need_value && n > 0 && !cols->value)
+      return fail(PDP_ERR_INVALID_ARG, "value column required for SUM/MEAN/VARIANCE");
+    if (!a->row_count) return fail(PDP_ERR_INVALID_ARG, "row_count accumulator required");
+    sps[c] = make_seg(b, plan.low, plan.pkb, cols->value != nullptr);
+    if (sps[c].want_count && !a->count) return fail(PDP_ERR_INVALID_ARG, "count accumulator required");
+    if (sps[c].xmode != kXNone && !a->x) return fail(PDP_ERR_INVALID_ARG, "x accumulator required");
+    if (sps[c].want_y && !a->y) return fail(PDP_ERR_INVALID_ARG, "y accumulator required");
+    accs[c] = AccPtrs{(unsigned long long*)a->row_count, (unsigned long long*)a->count, a->x, a->y};
+  }
   if (n > 0 && !cols->pk) return fail(PDP_ERR_INVALID_ARG, "pk column required");
   if (!bp->bounds_already_enforced && n > 0 && !cols->pid) return fail(PDP_ERR_INVALID_ARG, "pid column required");
-  if (!accp->row_count) return fail(PDP_ERR_INVALID_ARG, "row_count accumulator required");
-  const Plan plan = make_plan(n, std::max<int64_t>(U, 1), P);
-  SegParams sp = make_seg(bp, plan.low, plan.pkb, cols->value != nullptr);
-  if (sp.want_count && !accp->count) return fail(PDP_ERR_INVALID_ARG, "count accumulator required");
-  if (sp.xmode != kXNone && !accp->x) return fail(PDP_ERR_INVALID_ARG, "x accumulator required");
-  if (sp.want_y && !accp->y) return fail(PDP_ERR_INVALID_ARG, "y accumulator required");
-  AccPtrs acc{(unsigned long long*)accp->row_count, (unsigned long long*)accp->count, accp->x, accp->y};
+  SegParams sp = sps[0];
+  AccPtrs acc = accs[0];
   ctx->stats = pdp_stats{};
   ctx->stats.bucket_low_bits = plan.low;
 
-  HIP_TRY(hipMemsetAsync(acc.row_count, 0, (size_t)P * 8, stream));
-  if (acc.count) HIP_TRY(hipMemsetAsync(acc.count, 0, (size_t)P * 8, stream));
-  if (acc.x) HIP_TRY(hipMemsetAsync(acc.x, 0, (size_t)P * 8, stream));
-  if (acc.y) HIP_TRY(hipMemsetAsync(acc.y, 0, (size_t)P * 8, stream));
+  for (const AccPtrs& a : accs) {
+    HIP_TRY(hipMemsetAsync(a.row_count, 0, (size_t)P * 8, stream));
+    if (a.count) HIP_TRY(hipMemsetAsync(a.count, 0, (size_t)P * 8, stream));
+    if (a.x) HIP_TRY(hipMemsetAsync(a.x, 0, (size_t)P * 8, stream));
+    if (a.y) HIP_TRY(hipMemsetAsync(a.y, 0, (size_t)P * 8, stream));
+  }
   if (n == 0) return 0;
 
-  const Layout L = layout_for(n);
+  const Layout L = layout_for(n, sweep);
   if (!workspace || workspace_bytes < L.total) return fail(PDP_ERR_WORKSPACE, "workspace too small");
   char* ws = (char*)workspace;
   Rec* recs_a = (Rec*)(ws + L.recs_a);
@@ -1709,6 +1740,20 @@ int pdp_bound_accumulate(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_
   OvList ov{ranges, counters};
   BigList big{(unsigned long long*)(ws + L.big), L.big_cap};
   const int64_t seg_grid = (n + kSegTile - 1) / kSegTile;
+  Rec* alt = sweep ? (Rec*)(ws + L.recs_c) : sorted;
+  unsigned long long n_kept = 0;
+  for (int c = 0; c < nconf; ++c) {
+  bp = &bps[c];
+  sp = sps[c];
+  acc = accs[c];
+  sp.packed = sp.want_count && n < (1ll << 32);
+  if (c > 0) {
+    // fresh K2/KF counters; the kept-row count of the shared sort stays
+    unsigned long long reset[kCtrSweepCycles] = {};
+    reset[kCtrNKept] = n_kept;
+    HIP_TRY(hipMemcpyAsync(counters, reset, sizeof(reset), hipMemcpyHostToDevice, stream));
+    HIP_TRY(hipStreamSynchronize(stream));
+  }
   {
     ProfScope ps(ctx, PDP_STAGE_BUCKETS, stream);
     if (bp->max_partitions_contributed <= kLeanMaxL0 && !(sp.debug & kDebugBatchKernel)) {
@@ -1728,6 +1773,7 @@ int pdp_bound_accumulate(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_
   HIP_TRY(hipMemcpyAsync(host_ctr, counters, sizeof(host_ctr), hipMemcpyDeviceToHost, stream));
   HIP_TRY(hipStreamSynchronize(stream));
   ctx->stats.kept_rows_in = (int64_t)host_ctr[kCtrNKept];
+  n_kept = host_ctr[kCtrNKept];
   for (int i = 0; i < 4; ++i) ctx->stats.sweep_cycles[i] = (int64_t)host_ctr[kCtrSweepCycles + i];
   ctx->stats.sweep_tiles = (int64_t)host_ctr[kCtrSweepTiles];
   if (host_ctr[kCtrErr]) return fail(PDP_ERR_INTERNAL, "radix look-back timed out");
@@ -1746,8 +1792,8 @@ int pdp_bound_accumulate(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_
     HIP_TRY(hipStreamSynchronize(stream));
   }
   if (!rg.empty()) {
-    int rc = run_generic(ctx, sorted, spare, rg, plan, sp, bp, ks.num_pids, ks.num_parts, acc, hist, off, counters,
-                         status, status_bytes, workspace, stream);
+    int rc = run_generic(ctx, sorted, spare, alt, rg, plan, sp, bp, ks.num_pids, ks.num_parts, acc, hist, off,
+                         counters, status, status_bytes, workspace, stream);
     if (rc) return rc;
     unsigned long long err = 0;
     HIP_TRY(hipMemcpyAsync(&err, counters + kCtrErr, 8, hipMemcpyDeviceToHost, stream));
@@ -1759,7 +1805,20 @@ int pdp_bound_accumulate(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_
                        acc.count, P);
     HIP_TRY(hipGetLastError());
   }
+  }  // configurations
   return 0;
+}
+
+}  // namespace
+
+int pdp_bound_accumulate(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp,
+                         const pdp_accumulators* accp, void* workspace, size_t workspace_bytes, void* stream) {
+  return bound_impl(ctx, cols, bp, 1, accp, workspace, workspace_bytes, stream, false);
+}
+
+int pdp_bound_accumulate_sweep(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bps, int32_t num_configs,
+                               const pdp_accumulators* accs, void* workspace, size_t workspace_bytes, void* stream) {
+  return bound_impl(ctx, cols, bps, num_configs, accs, workspace, workspace_bytes, stream, true);
 }
 
 int pdp_release(pdp_ctx* ctx, const pdp_accumulators* accp, int64_t P, int64_t pk_offset,

@@ -7,7 +7,7 @@ device memory and streams only; all compute is in the HIP library.
 import ctypes
 import dataclasses
 import secrets
-from typing import Optional, Sequence
+from typing import List, Optional, Sequence
 
 from . import native
 
@@ -101,27 +101,34 @@ class HipExecutor:
             self._ws = self.torch.empty(max(nbytes, 256), dtype=self.torch.uint8, device=self.device)
         return self._ws
 
-    def accumulate(self, pid, pk, value, num_privacy_ids: int, num_partitions: int, cfg: BoundConfig,
-                   acc: Optional[Accumulators] = None) -> Accumulators:
-        """pdp_bound_accumulate on int64 pid/pk and float64 value device tensors."""
+    def _columns(self, pid, pk, value, num_privacy_ids, num_partitions):
         torch = self.torch
         n = int(pk.numel())
         for t, dt in ((pid, torch.int64), (pk, torch.int64), (value, torch.float64)):
             if t is not None:
                 assert t.device == self.device and t.dtype == dt and t.is_contiguous(), (t.device, t.dtype)
                 assert t.numel() == n
-        cols = native.Columns(_ptr(pid), _ptr(pk), _ptr(value), n, int(max(num_privacy_ids, 1)),
+        return native.Columns(_ptr(pid), _ptr(pk), _ptr(value), n, int(max(num_privacy_ids, 1)),
                               int(num_partitions))
+
+    @staticmethod
+    def _bound_params(cfg: BoundConfig):
         seed = cfg.sampling_seed if cfg.sampling_seed is not None else secrets.randbits(64)
-        bp = native.BoundParams(
+        return native.BoundParams(
             cfg.metrics_mask, int(cfg.bounds_already_enforced), cfg.max_partitions_contributed,
             cfg.max_contributions_per_partition, int(cfg.min_value is not None),
             int(cfg.min_sum_per_partition is not None),
             float(cfg.min_value or 0.0), float(cfg.max_value or 0.0),
             float(cfg.min_sum_per_partition or 0.0), float(cfg.max_sum_per_partition or 0.0),
             seed, int(cfg.debug_force_fallback), int(cfg.debug_flags))
+
+    def accumulate(self, pid, pk, value, num_privacy_ids: int, num_partitions: int, cfg: BoundConfig,
+                   acc: Optional[Accumulators] = None) -> Accumulators:
+        """pdp_bound_accumulate on int64 pid/pk and float64 value device tensors."""
+        cols = self._columns(pid, pk, value, num_privacy_ids, num_partitions)
+        bp = self._bound_params(cfg)
         if acc is None:
-            acc = Accumulators(torch, num_partitions, self.device, cfg.metrics_mask)
+            acc = Accumulators(self.torch, num_partitions, self.device, cfg.metrics_mask)
         nbytes = ctypes.c_size_t(0)
         native.check(self.lib.pdp_workspace_size(ctypes.byref(cols), ctypes.byref(bp), ctypes.byref(nbytes)),
                      "pdp_workspace_size")
@@ -131,6 +138,29 @@ class HipExecutor:
                                                    ctypes.c_void_p(ws.data_ptr()), ws.numel(), self.stream_handle),
                      "pdp_bound_accumulate")
         return acc
+
+    def accumulate_sweep(self, pid, pk, value, num_privacy_ids: int, num_partitions: int,
+                         cfgs: Sequence[BoundConfig]) -> List[Accumulators]:
+        """pdp_bound_accumulate_sweep: one sort by privacy id, then bounding +
+        accumulation per configuration (utility-analysis sweep over bounding
+        parameters, analysis/utility_analysis_engine.py:88-173).  Result c
+        equals accumulate(..., cfgs[c])."""
+        cols = self._columns(pid, pk, value, num_privacy_ids, num_partitions)
+        k = len(cfgs)
+        if k == 0:
+            return []
+        bps = (native.BoundParams * k)(*[self._bound_params(c) for c in cfgs])
+        out = [Accumulators(self.torch, num_partitions, self.device, c.metrics_mask) for c in cfgs]
+        accs = (native.Accumulators * k)(*[a.as_struct() for a in out])
+        nbytes = ctypes.c_size_t(0)
+        native.check(self.lib.pdp_sweep_workspace_size(ctypes.byref(cols), ctypes.byref(nbytes)),
+                     "pdp_sweep_workspace_size")
+        ws = self._workspace(nbytes.value)
+        native.check(self.lib.pdp_bound_accumulate_sweep(self.ctx, ctypes.byref(cols), bps, k, accs,
+                                                         ctypes.c_void_p(ws.data_ptr()), ws.numel(),
+                                                         self.stream_handle),
+                     "pdp_bound_accumulate_sweep")
+        return out
 
     def release(self, acc: Accumulators, cfg: ReleaseConfig, bounds: BoundConfig, pk_offset: int = 0,
                 num_partitions: Optional[int] = None, offset_in_acc: int = 0):

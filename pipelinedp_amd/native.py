@@ -70,6 +70,9 @@ SIGNATURES = [
                                    ctypes.POINTER(ctypes.c_size_t)]),
     ("pdp_bound_accumulate", c_i32, [c_vp, ctypes.POINTER(Columns), ctypes.POINTER(BoundParams),
                                      ctypes.POINTER(Accumulators), c_vp, ctypes.c_size_t, c_vp]),
+    ("pdp_sweep_workspace_size", c_i32, [ctypes.POINTER(Columns), ctypes.POINTER(ctypes.c_size_t)]),
+    ("pdp_bound_accumulate_sweep", c_i32, [c_vp, ctypes.POINTER(Columns), ctypes.POINTER(BoundParams), c_i32,
+                                           ctypes.POINTER(Accumulators), c_vp, ctypes.c_size_t, c_vp]),
     ("pdp_release", c_i32, [c_vp, ctypes.POINTER(Accumulators), c_i64, c_i64, ctypes.POINTER(ReleaseParams),
                             ctypes.POINTER(Outputs), c_vp]),
     ("pdp_metric_fields", c_i32, [c_i32, ctypes.POINTER(c_i32)]),
