@@ -32,7 +32,12 @@ WORKLOADS = {
                cpu_sample=12e6),
     "c4": dict(rows=5e8, partitions=5e7, pids=1.25e7, zipf=1.1, l0=32, linf=4, public=False, metrics="mean",
                cpu_sample=5e5),  # the oracle's O(P) release dominates at P=5e7
+    # c5: utility-analysis sweep, COUNT under 64 bounding configs (L0 x Linf) over 1e8 rows;
+    # one sort by privacy id, then bounding + accumulation per config (pdp_bound_accumulate_sweep).
+    "c5": dict(rows=1e8, partitions=1e5, pids=1e6, zipf=1.1, l0=0, linf=0, public=True, metrics="count",
+               cpu_sample=2e5),
 }
+SWEEP = [(l0, linf) for l0 in (1, 2, 4, 8, 16, 32, 64, 128) for linf in range(1, 9)]
 
 
 def parse():
@@ -98,6 +103,14 @@ def cpu_baseline(args, P):
     U = max(1, int(args.pids * m / args.rows))
     pid, pk, val = o.synth_rows(m, U, P, seed=args.seed, zipf_s=args.zipf)
     bp = o.BoundParams(args.l0, args.linf, 0.0, 10.0)
+    if WORKLOADS[args.workload]["metrics"] == "count":  # c5 sweep: bounding + COUNT per config
+        t0 = time.perf_counter()
+        for i, (l0, linf) in enumerate(SWEEP):
+            o.bound_and_accumulate(pid, pk, val, P, o.BoundParams(l0, linf), "hash", seed=i)
+        dt = time.perf_counter() - t0
+        return {"value": m / dt, "unit": "rows/s", "cores": 1, "kind": "port",
+                "sample": f"c5: {m} rows, {U} privacy ids, {P} Zipf({args.zipf}) partitions, {len(SWEEP)} "
+                          f"bounding configs; numpy oracle on 1 host core, {dt:.1f} s"}
     if WORKLOADS[args.workload]["public"]:
         spec = o.ReleaseSpec(("count", "sum"), "laplace", {"count": (0.5, 0.0), "sum": (0.5, 0.0)}, None)
     else:
@@ -137,7 +150,12 @@ def main():
     pid, pk, val = ex.generate(n, U, P, seed=args.seed, zipf_s=args.zipf, lo=0.0, hi=10.0, row_offset=rank * n)
     public = WORKLOADS[args.workload]["public"]
     count_sum = WORKLOADS[args.workload]["metrics"] == "count_sum"
+    sweep = WORKLOADS[args.workload]["metrics"] == "count"
     mask = native.METRIC_COUNT | native.METRIC_SUM | (0 if count_sum else native.METRIC_MEAN)
+    if sweep:
+        mask = native.METRIC_COUNT
+        sweep_cfgs = [BoundConfig(mask, l0, linf, sampling_seed=args.seed + 1 + i) for i, (l0, linf) in
+                      enumerate(SWEEP)]
     bounds = BoundConfig(mask, args.l0, args.linf, 0.0, 10.0, sampling_seed=args.seed + 1,
                          debug_flags=args.debug_flags)
     # NaiveBudgetAccountant(eps=1, delta=1e-6): MeanCombiner (Laplace) eps 0.5, selection eps 0.5 delta 1e-6
@@ -154,6 +172,9 @@ def main():
     fields = native.metric_fields(mask)
 
     def step():
+        if sweep:
+            accs = ex.accumulate_sweep(pid, pk, val, U, P, sweep_cfgs)
+            return (accs[-1].row_count,)
         if world is not None:
             return world.aggregate(ex, pid, pk, val, U, P, bounds, rel, gather=False)
         acc = ex.accumulate(pid, pk, val, U, P, bounds)
@@ -223,7 +244,11 @@ def main():
             "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f64",
             "data": "synthetic (on-device Philox generator, oracle/pdp_oracle.py:synth_rows)",
-            "config": {"workload": f"{args.workload}: DP {'COUNT+SUM' if count_sum else 'COUNT+SUM+MEAN'}, "
+            "config": {"workload": (f"c5: bounding sweep, COUNT under {len(SWEEP)} (L0, Linf) configs "
+                                    f"(L0 1..128 x Linf 1..8), {n:.2e} rows/GPU, {U:.1e} privacy ids, {P:.1e} "
+                                    f"Zipf({args.zipf}) partitions, one sort + {len(SWEEP)} bound/accumulate passes; "
+                                    f"value = input rows/s for the whole sweep") if sweep else
+                                   f"{args.workload}: DP {'COUNT+SUM' if count_sum else 'COUNT+SUM+MEAN'}, "
                                    f"{n:.2e} rows/GPU, {U:.1e} privacy ids/GPU, {P:.1e} "
                                    f"{'public uniform' if public else f'Zipf({args.zipf})'} partitions, "
                                    f"L0={args.l0}, Linf={args.linf}, [0,10], Laplace, "
