@@ -1759,7 +1759,8 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
     if (bp->max_partitions_contributed <= kLeanMaxL0 && !(sp.debug & kDebugBatchKernel)) {
       const int64_t waves = (n + kLeanChunk - 1) / kLeanChunk;
       const int64_t blocks = (waves + 3) / 4 < kLeanMaxBlocks ? (waves + 3) / 4 : kLeanMaxBlocks;
-      hipLaunchKernelGGL(k_lean, dim3((unsigned)blocks), dim3(256), 0, stream, sorted, counters,
+      hipLaunchKernelGGL(bp->max_partitions_contributed <= 64 ? k_lean<1> : k_lean<2>, dim3((unsigned)blocks),
+                         dim3(256), 0, stream, sorted, counters,
                          (int)kCtrNKept, sp, acc, ov, big, (int)bp->debug_force_fallback);
     } else {
       hipLaunchKernelGGL(k_segments, dim3((unsigned)seg_grid), dim3(kThreads), 0, stream, sorted, counters,

@@ -71,7 +71,9 @@ CONFIGS = [
     (30000, 1000, 3, 0.0, 2, 8, (0.0, 10.0), None, 1 | 2),  # groups of > 4 kept rows (wave-sum path)
     (40000, 500, 3000, 1.1, 32, 2, (0.0, 10.0), None, 1 | 2 | 4 | 16),  # c4-like L0=32, binding for some pids
     (30000, 250, 20000, 0.0, 64, 3, (-1.0, 9.0), None, 1 | 4 | 8 | 16),  # L0=64: every lane holds a kept group
-    (30000, 250, 20000, 0.0, 65, 3, (0.0, 10.0), None, 1 | 2),  # L0 > 64: batch kernel
+    (30000, 250, 20000, 0.0, 65, 3, (0.0, 10.0), None, 1 | 2),  # L0 > 64: lean with two output slots per lane
+    (30000, 200, 20000, 0.0, 128, 2, (0.0, 10.0), None, 1 | 4 | 16),  # largest L0 of the lean kernel
+    (30000, 200, 20000, 0.0, 129, 2, (0.0, 10.0), None, 1 | 2 | 16),  # L0 > 128: batch kernel
 ]
 
 
