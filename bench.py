@@ -27,9 +27,9 @@ PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 # c4: high-cardinality stress, one GPU's shard of 4e9 rows / 5e7 Zipf partitions, L0=32.
 WORKLOADS = {
     "c3": dict(rows=1e9, partitions=1e6, pids=1e7, zipf=1.1, l0=4, linf=2, public=False, metrics="mean",
-               cpu_sample=12e6),
+               cpu_sample=6e6),  # CPU baseline rows per host core
     "c2": dict(rows=1e8, partitions=1e5, pids=1e6, zipf=0.0, l0=8, linf=4, public=True, metrics="count_sum",
-               cpu_sample=12e6),
+               cpu_sample=6e6),
     "c4": dict(rows=5e8, partitions=5e7, pids=1.25e7, zipf=1.1, l0=32, linf=4, public=False, metrics="mean",
                cpu_sample=5e5),  # the oracle's O(P) release dominates at P=5e7
     # c5: utility-analysis sweep, COUNT under 64 bounding configs (L0 x Linf) over 1e8 rows;
@@ -96,37 +96,131 @@ def copy_peak_gbs(torch, nbytes=8 << 30, iters=5):
     return round(gbs, 1)
 
 
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
+_SHM = {}  # fork-shared sample buffers of the CPU baseline workers
+
+
+def _cpu_gen(task):
+    """Worker: rows [lo, hi) of the synthetic sample into the shared buffers."""
+    import numpy as np
+    import pdp_oracle as o
+    lo, hi, U, P, seed, zipf = task
+    pid, pk, val = o.synth_rows(hi - lo, U, P, seed=seed, zipf_s=zipf, row_offset=lo)
+    _SHM["pid"][lo:hi] = pid
+    _SHM["pk"][lo:hi] = pk
+    _SHM["val"][lo:hi] = val
+    return hi - lo
+
+
+def _cpu_bound(task):
+    """Worker: bound + accumulate the rows of privacy-id shard w (pid % W == w);
+    returns the touched partitions' accumulators (sparse)."""
+    import numpy as np
+    import pdp_oracle as o
+    w, W, P, l0, linf, seed = task
+    pid, pk, val = _SHM["pid"], _SHM["pk"], _SHM["val"]
+    mine = (pid % W) == w
+    acc = o.bound_and_accumulate(pid[mine], pk[mine], val[mine], P, o.BoundParams(l0, linf, 0.0, 10.0), "hash",
+                                 seed=seed)
+    idx = np.flatnonzero(acc.row_count)
+    return idx, acc.row_count[idx], acc.count[idx], acc.sum[idx], acc.nsum[idx]
+
+
 def cpu_baseline(args, P):
+    """BASELINE.md CPU plan item 3: the numpy restatement (oracle/pdp_oracle.py)
+    on the host cores of this box, privacy ids sharded over a process pool
+    (the reference's LocalBackend is single-threaded and cannot travel here).
+    Runs before the GPU is initialised (fork pool).  The sample is generated
+    in parallel outside the timed region; timed: shard + bound + accumulate
+    per worker, merge, selection + noise."""
+    import mmap
+    import multiprocessing as mp
+
+    import numpy as np
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pdp_oracle as o  # checker / baseline only
-    m = int(args.cpu_sample)
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except AttributeError:
+        cores = os.cpu_count() or 1
+    W = max(1, min(16, cores))  # the GPU box's CPU share is 16 cores per GPU
+    m = int(args.cpu_sample) * W
     U = max(1, int(args.pids * m / args.rows))
-    pid, pk, val = o.synth_rows(m, U, P, seed=args.seed, zipf_s=args.zipf)
-    bp = o.BoundParams(args.l0, args.linf, 0.0, 10.0)
-    if WORKLOADS[args.workload]["metrics"] == "count":  # c5 sweep: bounding + COUNT per config
+    for name, dt in (("pid", np.int64), ("pk", np.int64), ("val", np.float64)):
+        _SHM[name] = np.frombuffer(mmap.mmap(-1, max(8 * m, 8)), dtype=dt, count=m)
+    ctx = mp.get_context("fork")
+    metrics = WORKLOADS[args.workload]["metrics"]
+    with ctx.Pool(W) as pool:
+        bounds = np.linspace(0, m, W + 1).astype(np.int64)
+        pool.map(_cpu_gen, [(int(bounds[i]), int(bounds[i + 1]), U, P, args.seed, args.zipf) for i in range(W)])
         t0 = time.perf_counter()
-        for i, (l0, linf) in enumerate(SWEEP):
-            o.bound_and_accumulate(pid, pk, val, P, o.BoundParams(l0, linf), "hash", seed=i)
+        parts = pool.map(_cpu_bound, [(w, W, P, args.l0, args.linf, 1) for w in range(W)])
+        rc, cnt, sm, ns = (np.zeros(P, np.int64), np.zeros(P, np.int64), np.zeros(P), np.zeros(P))
+        for idx, a, b, c, d in parts:
+            rc[idx] += a
+            cnt[idx] += b
+            sm[idx] += c
+            ns[idx] += d
+        acc = o.Accumulators(rc, cnt, sm, ns, np.zeros(P))
+        bp = o.BoundParams(args.l0, args.linf, 0.0, 10.0)
+        if WORKLOADS[args.workload]["public"]:
+            spec = o.ReleaseSpec(("count", "sum"), "laplace", {"count": (0.5, 0.0), "sum": (0.5, 0.0)}, None)
+        else:
+            spec = o.ReleaseSpec(("mean", "count", "sum"), "laplace", {"mean": (0.5, 0.0)}, "truncated_geometric",
+                                 (0.5, 1e-6))
+        if metrics != "count":
+            o.release(acc, bp, spec, seed=2)
         dt = time.perf_counter() - t0
-        return {"value": m / dt, "unit": "rows/s", "cores": 1, "kind": "port",
-                "sample": f"c5: {m} rows, {U} privacy ids, {P} Zipf({args.zipf}) partitions, {len(SWEEP)} "
-                          f"bounding configs; numpy oracle on 1 host core, {dt:.1f} s"}
-    if WORKLOADS[args.workload]["public"]:
-        spec = o.ReleaseSpec(("count", "sum"), "laplace", {"count": (0.5, 0.0), "sum": (0.5, 0.0)}, None)
-    else:
-        spec = o.ReleaseSpec(("mean", "count", "sum"), "laplace", {"mean": (0.5, 0.0)}, "truncated_geometric",
-                             (0.5, 1e-6))
-    t0 = time.perf_counter()
-    acc = o.bound_and_accumulate(pid, pk, val, P, bp, "hash", seed=1)
-    o.release(acc, bp, spec, seed=2)
-    dt = time.perf_counter() - t0
-    return {"value": m / dt, "unit": "rows/s", "cores": 1, "kind": "port",
-            "sample": f"{args.workload}: {m} rows, {U} privacy ids, {P} Zipf({args.zipf}) partitions; numpy oracle "
-                      f"(oracle/pdp_oracle.py) on 1 host core, {dt:.1f} s"}
+    for k in list(_SHM):
+        del _SHM[k]
+    return {"value": m / dt, "unit": "rows/s", "cores": W, "kind": "port", "plan_item": 3,
+            "host_cpus_visible": os.cpu_count(), "cpu_model": _cpu_model(),
+            "sample": f"{args.workload}: {m} rows ({int(args.cpu_sample)} per core), {U} privacy ids, {P} "
+                      f"{'public uniform' if WORKLOADS[args.workload]['public'] else f'Zipf({args.zipf})'} "
+                      f"partitions, L0={args.l0}, Linf={args.linf}; numpy restatement (oracle/pdp_oracle.py), "
+                      f"privacy ids sharded over {W} processes, merge + selection + noise on one; {dt:.1f} s"}
+
+
+def launch_ranks(args):
+    """`--gpus N` without a torch.distributed launcher: start N rank processes
+    (one per GPU, LOCAL_RANK = rank) from this parent, which never touches the
+    GPU, and return the worst exit code.  Rank 0 prints the JSON line."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus), LOCAL_WORLD_SIZE=str(args.gpus),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    return max(abs(p.wait()) for p in procs)
 
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
+    world_size = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    cpu = None
+    if rank == 0 and world_size == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args, int(args.partitions))  # before the GPU is initialised (fork pool)
+
     import torch
     import torch.distributed as dist
 
@@ -134,9 +228,6 @@ def main():
     from pipelinedp_amd.distributed import World
     from pipelinedp_amd.executor import BoundConfig, HipExecutor, ReleaseConfig
 
-    world_size = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
     world = None
     if world_size > 1:
@@ -148,6 +239,8 @@ def main():
     U = int(args.pids)
     ex = HipExecutor(local)
     pid, pk, val = ex.generate(n, U, P, seed=args.seed, zipf_s=args.zipf, lo=0.0, hi=10.0, row_offset=rank * n)
+    # Multi-GPU: rank r's rows carry its own privacy ids (global id = r * U + local id), so every privacy id
+    # lives on one rank (pid-sharded input, weak scaling); the sort uses the dense local ids.
     public = WORKLOADS[args.workload]["public"]
     count_sum = WORKLOADS[args.workload]["metrics"] == "count_sum"
     sweep = WORKLOADS[args.workload]["metrics"] == "count"
@@ -184,7 +277,7 @@ def main():
         step()
     torch.cuda.synchronize()
     st = ex.stats()
-    kept_rows = int(st.kept_rows_in)
+    rows_after_public_filter = int(st.kept_rows_in)
     if not args.no_profile:
         ex.profile(True)
         ex.profile_read(reset=True)
@@ -214,30 +307,33 @@ def main():
                 stages[s] = {"ms_per_launch": ms / cnt, "launches_per_step": cnt / args.steps}
         dom = max(stages, key=lambda s: stages[s]["ms_per_launch"] * stages[s]["launches_per_step"])
         nb = (P + world_size - 1) // world_size if world else P
-        b = stage_bytes(dom, n, kept_rows, nb, len(fields))
+        b = stage_bytes(dom, n, rows_after_public_filter, nb, len(fields))
         ach = b / (stages[dom]["ms_per_launch"] * 1e-3) / 1e9
-        traffic = None
-        pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-        if os.path.exists(pmc_path):
-            pmc = json.load(open(pmc_path))
-            if pmc.get("config_rows") == n and dom in pmc.get("bytes_per_launch", {}):
-                traffic = pmc["bytes_per_launch"][dom]
         roofline = {"bound": "hbm", "kernel": dom, "achieved": round(ach, 1), "peak": PEAK_HBM_GBS,
-                    "unit": "GB/s", "frac": round(ach / PEAK_HBM_GBS, 4), "traffic": traffic,
-                    "algorithmic_bytes_per_launch": b}
+                    "unit": "GB/s", "frac": round(ach / PEAK_HBM_GBS, 4), "traffic": None,
+                    "traffic_note": "HBM bytes need a separate rocprofv3 --pmc pass (FETCH_SIZE x2 on gfx950 + "
+                                    "WRITE_SIZE), committed under profiles/; not measurable inside this run",
+                    "algorithmic_bytes_per_launch": b,
+                    "ms_per_launch_source": "hipEvents on the launch stream, averaged over the timed steps"}
         for s in stages:
-            bs = stage_bytes(s, n, kept_rows, nb, len(fields))
+            bs = stage_bytes(s, n, rows_after_public_filter, nb, len(fields))
             if bs:
                 stages[s]["achieved_GBs"] = round(bs / (stages[s]["ms_per_launch"] * 1e-3) / 1e9, 1)
+
+    # bounding statistics of one more (untimed) run: rows and (pid, pk) pairs kept
+    kept = {}
+    if not sweep:
+        acc = ex.accumulate(pid, pk, val, U, P, bounds)
+        kept = {"rows_kept_after_bounding": int(acc.count.sum().item()) if acc.count is not None else None,
+                "pairs_kept_after_bounding": int(acc.row_count.sum().item())}
+        del acc
 
     rows_per_s = n * world_size * args.steps / elapsed
     copy_gbs = copy_peak_gbs(torch) if rank == 0 and not args.no_profile else None
     if roofline is not None:
         roofline["copy_peak_measured"] = copy_gbs
-    cpu = None
-    if rank == 0 and world_size == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args, P)
     if rank == 0:
+        e2e = rows_per_s * 24 / 1e9
         line = {
             "metric": "input rows/sec (node) for DP COUNT+SUM+MEAN, 1B rows/1M partitions; % HBM peak",
             "value": rows_per_s, "unit": "rows/s", "n_gpus": world_size, "steps": args.steps,
@@ -256,8 +352,22 @@ def main():
                                    f", eps=1 delta=1e-6",
                        "rows_per_gpu": n, "partitions": P, "privacy_ids_per_gpu": U,
                        "parallelism": f"pid-sharded x{world_size}" + (" + RCCL reduce-scatter" if world else "")},
-            "roofline": roofline, "cpu_baseline": cpu,
-            "kernels": stages, "kept_rows": kept_rows, "kept_partitions_rank0": kept_parts,
+            "roofline": roofline,
+            "roofline_e2e": {"definition": "rows/s x 24 B/row (int64 pid + int64 pk + f64 value read once) / "
+                                           "8 TB/s (BASELINE.md:61-64)",
+                             "bytes_per_row": 24, "achieved": round(e2e, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                             "frac": round(e2e / PEAK_HBM_GBS, 4)},
+            "cpu_baseline": cpu,
+            "reference_cpu_carried": {"value": 66.1e3, "unit": "rows/s", "cores": 1, "plan_item": 1,
+                                      "kind": "reference LocalBackend (stubbed PyDP: identity noise, keep-all)",
+                                      "where": "measured in the build container, NOT on this box (the reference "
+                                               "never ships here); carried from BASELINE.md:28",
+                                      "config": "COUNT+SUM+MEAN, 1e6 rows, 1e5 users, 17,770 Zipf(1.1) partitions, "
+                                                "L0=2, Linf=1"},
+            "fp64_sums": "per-partition fp64 sums use fp64 atomics: summation order, hence the last bits, vary run "
+                         "to run; counts and keep decisions are exact and deterministic",
+            "kernels": stages, "rows_after_public_filter": rows_after_public_filter, **kept,
+            "kept_partitions_rank0": kept_parts,
             "sort_passes": int(st.sort_passes), "bucket_low_bits": int(st.bucket_low_bits),
             "fallback_rows": int(st.fallback_rows),
         }

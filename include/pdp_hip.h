@@ -199,6 +199,20 @@ int pdp_truncated_geometric_table(double eps, double delta, int64_t max_partitio
 int pdp_selection_threshold(int32_t selection, double eps, double delta, int64_t max_partitions,
                             double* threshold, double* scale);
 
+/* Multi-GPU ingestion of rows that are not sharded by privacy id: the device
+ * side of the reference's group-by-pid shuffles (BeamBackend / SparkRDDBackend
+ * / LocalBackend.group_by_key, pipeline_dp/pipeline_backend.py:261, 401,
+ * 476-485).  Stable counting sort of the rows by destination rank
+ * shard_of(pid) = splitmix64(pid ^ 0x9E3779B97F4A7C15) % world_size into
+ * out_pid / out_pk / out_value (device, num_rows each; rank 0's rows first,
+ * input order kept within a rank); rows_per_rank[world_size] is HOST memory.
+ * The caller then moves the runs with an RCCL all-to-all.  value / out_value
+ * may both be NULL.  world_size <= 64. */
+int pdp_shard_workspace_size(int64_t num_rows, int32_t world_size, size_t* bytes);
+int pdp_shard_rows(pdp_ctx* ctx, const pdp_columns* cols, int32_t world_size, int64_t* out_pid, int64_t* out_pk,
+                   double* out_value, int64_t* rows_per_rank, void* workspace, size_t workspace_bytes,
+                   void* stream);
+
 /* Synthetic workload (bench / tests): rows [row_offset, row_offset+n) of the
  * generator specified in oracle/pdp_oracle.py:synth_rows. */
 int pdp_generate_synthetic(int64_t* pid, int64_t* pk, double* value, int64_t n, int64_t row_offset,

@@ -13,8 +13,9 @@ Parity pinning: the restatement is checked against
     (``tests/golden/reference_known_answers.json``), e.g. the PyDP Gaussian
     sigma values and truncated-geometric keep probabilities.
 LAPLACE_THRESHOLDING / GAUSSIAN_THRESHOLDING thresholds and the k>1
-adjustment of truncated geometric are "parity unpinned" (PyDP is absent and
-the reference tests only mock it).
+per-partition (eps / k, 1 - (1 - delta)^(1/k)) adjustment shared by all three
+selection strategies are "parity unpinned" (PyDP is absent and the reference
+tests only mock it).
 
 Each function cites the reference file:line it restates.
 
@@ -29,7 +30,10 @@ DESIGN.md "Randomness"):
     ``sampler='numpy'`` draws uniform subsets with numpy like LocalBackend
     (``pipeline_backend.py:504-520``).
   * noise / selection draws use Philox4x32-10 keyed by the 64-bit noise seed
-    with counter (pk_lo, pk_hi, stream, 0).
+    with counter (pk_lo, pk_hi, stream, 0); Laplace noise is a two-sided
+    geometric on the grid 2^(ceil(log2 b) - 40), Gaussian noise is rounded to
+    that grid, and the released value is snapped to it (granularity
+    snapping as in PyDP's secure mechanisms; not PyDP's implementation).
 """
 import math
 from dataclasses import dataclass, field
@@ -202,17 +206,49 @@ def philox_uniforms(seed, idx, stream):
     return _uniform53(x0, x1), _uniform53(x2, x3)
 
 
-def unit_laplace(seed, idx, stream):
-    """Laplace(0, 1) by inverse CDF of the first Philox uniform."""
-    u, _ = philox_uniforms(seed, idx, stream)
-    d = u - 0.5
-    return -np.sign(d) * np.log1p(-2.0 * np.abs(d))
+def _uniform64(hi, lo):
+    """Uniform in (0,1) from a 64-bit word, exact near 0 (pdp_rng.h:uniform64)."""
+    w = (hi << np.uint64(32)) | lo
+    big = w >= np.uint64(1 << 53)
+    top = ((w >> np.uint64(11)).astype(np.float64) + 0.5) * (1.0 / 9007199254740992.0)
+    low = (np.where(big, np.uint64(0), w).astype(np.float64) + 0.5) * 5.421010862427522e-20
+    return np.where(big, top, low)
 
 
-def unit_gaussian(seed, idx, stream):
-    """N(0, 1) by Box-Muller on the two Philox uniforms."""
-    u1, u2 = philox_uniforms(seed, idx, stream)
-    return np.sqrt(-2.0 * np.log(u1)) * np.cos(2.0 * math.pi * u2)
+def noise_grid(scale):
+    """Noise grid 2^(ceil(log2 scale) - 40) (pdp_rng.h:noise_grid)."""
+    m, e = math.frexp(scale)
+    return math.ldexp(1.0, (e - 1 if m == 0.5 else e) - 40)
+
+
+def laplace_on_grid(seed, idx, stream, b, g):
+    """Laplace(0, b) as a two-sided geometric on the grid g: g (G1 - G2),
+    G_i = floor(E_i b / g), E_i = -log(u_i) from the two 64-bit Philox words."""
+    idx = _u64(idx)
+    seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+    x0, x1, x2, x3 = philox4x32_10(idx & _M32, idx >> np.uint64(32), np.uint64(stream), np.uint64(0),
+                                   np.uint64(seed & 0xFFFFFFFF), np.uint64(seed >> 32))
+    e1 = -np.log(_uniform64(x0, x1))
+    e2 = -np.log(_uniform64(x2, x3))
+    return g * (np.floor(e1 * (b / g)) - np.floor(e2 * (b / g)))
+
+
+def gaussian_on_grid(seed, idx, stream, sigma, g):
+    """N(0, sigma^2) by Box-Muller, rounded to the grid g."""
+    idx = _u64(idx)
+    seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+    x0, x1, x2, x3 = philox4x32_10(idx & _M32, idx >> np.uint64(32), np.uint64(stream), np.uint64(0),
+                                   np.uint64(seed & 0xFFFFFFFF), np.uint64(seed >> 32))
+    z = np.sqrt(-2.0 * np.log(_uniform64(x0, x1))) * np.cos(2.0 * math.pi * _uniform53(x2, x3))
+    return g * np.rint(sigma * z / g)
+
+
+def add_snapped_noise(kind, value, seed, idx, stream, scale):
+    """value + noise, both on the grid of `scale` (pdp_rng.h:add_snapped_noise)."""
+    g = noise_grid(scale)
+    z = laplace_on_grid(seed, idx, stream, scale, g) if kind == "laplace" else \
+        gaussian_on_grid(seed, idx, stream, scale, g)
+    return g * np.rint(np.asarray(value, dtype=np.float64) / g) + z
 
 
 # ----------------------------------------------------------------------------
@@ -280,16 +316,28 @@ def gaussian_sigma(eps, delta, l2_sensitivity):
     return hi * l2_sensitivity
 
 
+def adjusted_delta(delta, k):
+    """Per-partition delta over k = max_partitions_contributed partitions:
+    1 - (1 - delta)^(1/k) (k independent decisions compose to delta); the
+    one adjustment of all three selection strategies here.  Parity unpinned
+    for k > 1 (PyDP is absent; the reference pins only k = 1, where this is
+    delta).  Differs from delta / k by less than delta^2 / 2."""
+    if k <= 1:
+        return delta
+    return -math.expm1(math.log1p(-delta) / k)
+
+
 def truncated_geometric_table(eps, delta, max_partitions, max_len=1 << 22):
     """Keep probability p(n) of PyDP's truncated-geometric partition
     selection, n = 0..len-1; p(n) = 1 for n beyond the table.
     Recurrence (pinned for k=1 by analysis/tests/combiners_test.py:197-224):
       p(0) = 0; p(n) = min(e^eps p(n-1) + delta,
                            1 - e^-eps (1 - p(n-1) - delta), 1)
-    with eps, delta divided by k = max_partitions (k > 1: parity unpinned).
+    with eps / k and adjusted_delta(delta, k), k = max_partitions (k > 1:
+    parity unpinned).
     """
     e = eps / max_partitions
-    d = delta / max_partitions
+    d = adjusted_delta(delta, max_partitions)
     ee = math.exp(e)
     eme = math.exp(-e)
     p = [0.0]
@@ -313,7 +361,7 @@ def truncated_geometric_keep_prob(n, eps, delta, max_partitions):
 def laplace_threshold(eps, delta, max_partitions):
     """LAPLACE_THRESHOLDING (PyDP LaplacePartitionSelection) — parity
     unpinned restatement.  Returns (threshold, diversity)."""
-    adj_delta = 1.0 - (1.0 - delta)**(1.0 / max_partitions)
+    adj_delta = adjusted_delta(delta, max_partitions)
     b = max_partitions / eps
     if adj_delta > 0.5:
         thr = 1.0 + b * math.log(2.0 * (1.0 - adj_delta))
@@ -333,7 +381,7 @@ def gaussian_threshold(eps, delta, max_partitions):
     thr_delta = delta / 2.0
     noise_delta = delta - thr_delta
     sigma = gaussian_sigma(eps, noise_delta, math.sqrt(max_partitions))
-    adj = 1.0 - (1.0 - thr_delta)**(1.0 / max_partitions)
+    adj = adjusted_delta(thr_delta, max_partitions)
     return 1.0 + sigma * _norm_ppf(1.0 - adj), sigma
 
 
@@ -537,11 +585,12 @@ class ReleaseSpec:
     max_rows_per_privacy_id: int = 1
 
 
-def _noise(seed, pk_idx, stream, kind, scale, enabled):
+def _noisy(value, seed, pk_idx, stream, kind, scale, enabled):
+    """value + snapped noise of `scale` (k_release: noisy); value if off."""
+    value = np.asarray(value, dtype=np.float64)
     if not enabled or scale == 0:
-        return np.zeros(len(pk_idx))
-    z = unit_laplace(seed, pk_idx, stream) if kind == "laplace" else unit_gaussian(seed, pk_idx, stream)
-    return scale * z
+        return value
+    return add_snapped_noise(kind, value, seed, pk_idx, stream, scale)
 
 
 def release(acc: Accumulators, bp: BoundParams, spec: ReleaseSpec, seed=0,
@@ -570,11 +619,10 @@ def release(acc: Accumulators, bp: BoundParams, spec: ReleaseSpec, seed=0,
         else:
             if spec.selection == "laplace":
                 thr, scale = laplace_threshold(eps, delta, L0)
-                z = unit_laplace(seed, idx, STREAM_SELECT)
             else:
                 thr, scale = gaussian_threshold(eps, delta, L0)
-                z = unit_gaussian(seed, idx, STREAM_SELECT)
-            keep = (nn > 0) & (nn + (scale * z if noise else 0.0) > thr)
+            v = _noisy(nn, seed, idx, STREAM_SELECT, spec.selection, scale, noise)
+            keep = (nn > 0) & (v > thr)
 
     def lin_sum_linf():
         if bp.min_value is not None:
@@ -585,20 +633,20 @@ def release(acc: Accumulators, bp: BoundParams, spec: ReleaseSpec, seed=0,
         eps, delta = spec.budgets["variance"]
         (ce, cd), (se, sd), (qe, qd) = equally_split_budget(eps, delta, 3)
         a, b = bp.min_value, bp.max_value
-        dp_count = acc.count + _noise(seed, idx, STREAM_MEAN_COUNT, kind, noise_scale(kind, ce, cd, L0, Linf), noise)
+        dp_count = _noisy(acc.count, seed, idx, STREAM_MEAN_COUNT, kind, noise_scale(kind, ce, cd, L0, Linf), noise)
         denom = np.maximum(1.0, dp_count)
         if a == b:
             dp_mean = np.full(P, float(a))
         else:
             mid = compute_middle(a, b)
-            dp_mean = (acc.nsum + _noise(seed, idx, STREAM_MEAN_NSUM, kind,
+            dp_mean = (_noisy(acc.nsum, seed, idx, STREAM_MEAN_NSUM, kind,
                                          noise_scale(kind, se, sd, L0, Linf * abs(mid - a)), noise)) / denom
         sa, sb = compute_squares_interval(a, b)
         if sa == sb:
             dp_msq = np.full(P, float(sa))
         else:
             msq = compute_middle(sa, sb)
-            dp_msq = (acc.nsumsq + _noise(seed, idx, STREAM_VAR_NSQ, kind,
+            dp_msq = (_noisy(acc.nsumsq, seed, idx, STREAM_VAR_NSQ, kind,
                                           noise_scale(kind, qe, qd, L0, Linf * abs(msq - sa)), noise)) / denom
         var = dp_msq - dp_mean**2
         if a != b:
@@ -614,12 +662,12 @@ def release(acc: Accumulators, bp: BoundParams, spec: ReleaseSpec, seed=0,
         eps, delta = spec.budgets["mean"]
         (ce, cd), (se, sd) = equally_split_budget(eps, delta, 2)
         a, b = bp.min_value, bp.max_value
-        dp_count = acc.count + _noise(seed, idx, STREAM_MEAN_COUNT, kind, noise_scale(kind, ce, cd, L0, Linf), noise)
+        dp_count = _noisy(acc.count, seed, idx, STREAM_MEAN_COUNT, kind, noise_scale(kind, ce, cd, L0, Linf), noise)
         if a == b:
             dp_mean = np.full(P, float(a))
         else:
             mid = compute_middle(a, b)
-            dp_mean = (acc.nsum + _noise(seed, idx, STREAM_MEAN_NSUM, kind,
+            dp_mean = (_noisy(acc.nsum, seed, idx, STREAM_MEAN_NSUM, kind,
                                          noise_scale(kind, se, sd, L0, Linf * abs(mid - a)), noise)) / np.maximum(1.0, dp_count)
             dp_mean = dp_mean + mid
         out["mean"] = dp_mean
@@ -630,17 +678,17 @@ def release(acc: Accumulators, bp: BoundParams, spec: ReleaseSpec, seed=0,
     else:
         if "count" in m:
             eps, delta = spec.budgets["count"]
-            out["count"] = acc.count + _noise(seed, idx, STREAM_COUNT, kind, noise_scale(kind, eps, delta, L0, Linf), noise)
+            out["count"] = _noisy(acc.count, seed, idx, STREAM_COUNT, kind, noise_scale(kind, eps, delta, L0, Linf), noise)
         if "sum" in m:
             eps, delta = spec.budgets["sum"]
             linf = lin_sum_linf()
             if linf == 0:
                 out["sum"] = np.zeros(P)
             else:
-                out["sum"] = acc.sum + _noise(seed, idx, STREAM_SUM, kind, noise_scale(kind, eps, delta, L0, linf), noise)
+                out["sum"] = _noisy(acc.sum, seed, idx, STREAM_SUM, kind, noise_scale(kind, eps, delta, L0, linf), noise)
     if "privacy_id_count" in m:
         eps, delta = spec.budgets["privacy_id_count"]
-        out["privacy_id_count"] = acc.row_count + _noise(seed, idx, STREAM_PID_COUNT, kind,
+        out["privacy_id_count"] = _noisy(acc.row_count, seed, idx, STREAM_PID_COUNT, kind,
                                                          noise_scale(kind, eps, delta, L0, Linf), noise)
     return keep, out
 

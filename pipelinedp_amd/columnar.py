@@ -23,6 +23,10 @@ class ColumnarData:
     value:       float64 values (None for COUNT / PRIVACY_ID_COUNT).
     partition_keys: optional original key of each dense partition id; when
                  given, public_partitions are expressed in this key space.
+    privacy_id_sharded: multi-GPU only -- every privacy id's rows are on one
+                 rank already (rank = distributed.shard_of(pid)), so no
+                 all-to-all shuffle is needed.  Ids must be GLOBAL (the same
+                 dense id means the same key on every rank).
     """
     partition: Any
     privacy_id: Any = None
@@ -30,6 +34,7 @@ class ColumnarData:
     num_partitions: Optional[int] = None
     num_privacy_ids: Optional[int] = None
     partition_keys: Optional[Sequence] = None
+    privacy_id_sharded: bool = False
 
     def __len__(self):
         return int(self.partition.shape[0]) if hasattr(self.partition, "shape") else len(self.partition)
@@ -62,27 +67,57 @@ def _unique_in_order(keys):
     return list(seen)
 
 
-def encode_rows(rows, extractors, public_partitions=None, need_pid=True, need_value=True) -> EncodedColumns:
+def _index_of(keys, raw):
+    """Dense ids of `raw` in the key list `keys` (-1 = absent)."""
+    import pandas as pd
+    if not len(raw):
+        return np.zeros(0, np.int64)
+    idx = pd.Index(keys, dtype=object) if len(keys) else pd.Index([], dtype=object)
+    return idx.get_indexer(pd.Index(raw, dtype=object)).astype(np.int64)
+
+
+def _global_keys(local_keys, world):
+    """One key dictionary for all ranks: every rank's keys (first-appearance
+    order) concatenated in rank order, deduplicated.  Ranks that
+    reduce-scatter dense per-partition accumulators must number partitions
+    identically."""
+    import torch.distributed as dist
+    gathered = [None] * world.size
+    dist.all_gather_object(gathered, list(local_keys), group=world.group)
+    return _unique_in_order(k for ks in gathered for k in ks)
+
+
+def encode_rows(rows, extractors, public_partitions=None, need_pid=True, need_value=True,
+                world=None) -> EncodedColumns:
     """Apply the extractors once per row and dictionary-encode.
 
     Partition ids: public partitions (deduplicated, in the given order) get
     ids [0, len(public)); rows of other partitions get -1 (dropped, like
     ``_drop_not_public_partitions`` dp_engine.py:283-293).  Without public
-    partitions ids follow first appearance.
+    partitions ids follow first appearance.  With a multi-rank ``world``
+    (``distributed.World``) the partition and privacy-id dictionaries are
+    agreed across ranks (``_global_keys``), so dense ids mean the same key
+    on every rank.
     """
     rows = rows if isinstance(rows, list) else list(rows)
+    multi = world is not None and world.size > 1
     pk_raw = [extractors.partition_extractor(r) for r in rows]
     if public_partitions is not None:
-        import pandas as pd
         keys = _unique_in_order(public_partitions)
-        idx = pd.Index(keys, dtype=object) if keys else pd.Index([], dtype=object)
-        pk = idx.get_indexer(pd.Index(pk_raw, dtype=object)).astype(np.int64) if rows else np.zeros(0, np.int64)
+        pk = _index_of(keys, pk_raw)
+    elif multi:
+        keys = _global_keys(_unique_in_order(pk_raw), world)
+        pk = _index_of(keys, pk_raw)
     else:
         pk, keys = _factorize(pk_raw) if rows else (np.zeros(0, np.int64), [])
     pid, U = None, 0
     if need_pid:
         pid_raw = [extractors.privacy_id_extractor(r) for r in rows]
-        if rows:
+        if multi:
+            pid_keys = _global_keys(_unique_in_order(pid_raw), world)
+            pid = _index_of(pid_keys, pid_raw)
+            U = len(pid_keys)
+        elif rows:
             pid, uniq = _factorize(pid_raw)
             U = len(uniq)
         else:

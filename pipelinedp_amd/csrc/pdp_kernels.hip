@@ -922,10 +922,12 @@ struct RelParams {
   uint64_t seed;
 };
 
-__device__ __forceinline__ double noise(const RelParams& rp, uint64_t idx, uint32_t stream, double scale) {
-  if (!rp.add_noise || scale == 0.0) return 0.0;
-  return scale * (rp.kind == PDP_NOISE_LAPLACE ? pdp::unit_laplace(rp.seed, idx, stream)
-                                               : pdp::unit_gaussian(rp.seed, idx, stream));
+// value + Laplace/Gaussian noise of `scale`, both snapped to the noise grid
+// (pdp_rng.h: add_snapped_noise); exact value when noise is off.
+__device__ __forceinline__ double noisy(const RelParams& rp, double value, uint64_t idx, uint32_t stream,
+                                        double scale) {
+  if (!rp.add_noise || scale == 0.0) return value;
+  return pdp::add_snapped_noise(rp.kind == PDP_NOISE_GAUSSIAN, value, rp.seed, idx, stream, scale);
 }
 
 __global__ void k_release(const unsigned long long* __restrict__ row_count,
@@ -950,32 +952,31 @@ __global__ void k_release(const unsigned long long* __restrict__ row_count,
           kp = p > 0.0;
         }
       } else {
-        double z = 0.0;
-        if (rp.add_noise)
-          z = rp.selection == PDP_SELECTION_LAPLACE_THRESHOLDING
-                  ? pdp::unit_laplace(rp.seed, gidx, pdp::kStreamSelect)
-                  : pdp::unit_gaussian(rp.seed, gidx, pdp::kStreamSelect);
-        kp = ((double)nn + rp.sel_scale * z) > rp.sel_thr;
+        const int gauss = rp.selection == PDP_SELECTION_GAUSSIAN_THRESHOLDING;
+        const double v = rp.add_noise
+                             ? pdp::add_snapped_noise(gauss, (double)nn, rp.seed, gidx, pdp::kStreamSelect, rp.sel_scale)
+                             : (double)nn;
+        kp = v > rp.sel_thr;
       }
     }
     keep[i] = kp;
     double f[5] = {0, 0, 0, 0, 0};  // variance, mean, count, sum, pid_count
     const int m = rp.metrics;
     if (m & (PDP_METRIC_VARIANCE | PDP_METRIC_MEAN)) {
-      const double dp_count = (double)(long long)count[i] + noise(rp, gidx, pdp::kStreamMeanCount, rp.s_mean_count);
+      const double dp_count = noisy(rp, (double)(long long)count[i], gidx, pdp::kStreamMeanCount, rp.s_mean_count);
       const double denom = dp_count > 1.0 ? dp_count : 1.0;
       double dp_mean;
       if (rp.mean_degenerate) {
         dp_mean = rp.a;
       } else {
-        dp_mean = (xs[i] + noise(rp, gidx, pdp::kStreamMeanNsum, rp.s_mean_nsum)) / denom;
+        dp_mean = noisy(rp, xs[i], gidx, pdp::kStreamMeanNsum, rp.s_mean_nsum) / denom;
       }
       if (m & PDP_METRIC_VARIANCE) {
         double msq;
         if (rp.sq_degenerate)
           msq = rp.sq_a;
         else
-          msq = (ys[i] + noise(rp, gidx, pdp::kStreamVarNsq, rp.s_var_nsq)) / denom;
+          msq = noisy(rp, ys[i], gidx, pdp::kStreamVarNsq, rp.s_var_nsq) / denom;
         f[0] = msq - dp_mean * dp_mean;
       }
       if (!rp.mean_degenerate) dp_mean += rp.mid;
@@ -983,12 +984,119 @@ __global__ void k_release(const unsigned long long* __restrict__ row_count,
       f[2] = dp_count;
       f[3] = dp_mean * dp_count;
     } else {
-      if (m & PDP_METRIC_COUNT)
-        f[2] = (double)(long long)count[i] + noise(rp, gidx, pdp::kStreamCount, rp.s_count);
-      if (m & PDP_METRIC_SUM) f[3] = rp.sum_zero ? 0.0 : xs[i] + noise(rp, gidx, pdp::kStreamSum, rp.s_sum);
+      if (m & PDP_METRIC_COUNT) f[2] = noisy(rp, (double)(long long)count[i], gidx, pdp::kStreamCount, rp.s_count);
+      if (m & PDP_METRIC_SUM) f[3] = rp.sum_zero ? 0.0 : noisy(rp, xs[i], gidx, pdp::kStreamSum, rp.s_sum);
     }
-    if (m & PDP_METRIC_PRIVACY_ID_COUNT) f[4] = (double)rc + noise(rp, gidx, pdp::kStreamPidCount, rp.s_pid);
+    if (m & PDP_METRIC_PRIVACY_ID_COUNT) f[4] = noisy(rp, (double)rc, gidx, pdp::kStreamPidCount, rp.s_pid);
     for (int k = 0; k < rp.nfields; ++k) out[(int64_t)k * P + i] = f[rp.field[k]];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Row shuffle by privacy-id shard (multi-GPU input not sharded by pid): the
+// device side of the reference's group-by-pid shuffles
+// (pipeline_backend.py:261, 401, 476-485).  Stable counting sort of the rows
+// by destination rank shard_of(pid) = splitmix64(pid ^ salt) % world; the
+// RCCL all-to-all then moves each destination's contiguous run.
+// ---------------------------------------------------------------------------
+
+constexpr int kShardMax = 64;
+constexpr int kShardChunk = 8192;  // rows per block, in order
+constexpr uint64_t kPidShardSalt = 0x9E3779B97F4A7C15ull;  // distributed.py:PID_SHARD_SALT
+
+__device__ __forceinline__ uint32_t shard_dest(int64_t pid, int world) {
+  return (uint32_t)(pdp::splitmix64((uint64_t)pid ^ kPidShardSalt) % (uint64_t)world);
+}
+
+__global__ __launch_bounds__(kThreads) void k_shard_count(const int64_t* __restrict__ pid, int64_t n, int world,
+                                                          unsigned long long* __restrict__ counts) {
+  __shared__ unsigned int c[kShardMax];
+  const int t = threadIdx.x;
+  if (t < kShardMax) c[t] = 0;
+  __syncthreads();
+  const int64_t lo = (int64_t)blockIdx.x * kShardChunk;
+  const int64_t hi = lo + kShardChunk < n ? lo + kShardChunk : n;
+  for (int64_t i = lo + t; i < hi; i += kThreads) atomicAdd(&c[shard_dest(pid[i], world)], 1u);
+  __syncthreads();
+  if (t < world) counts[(size_t)blockIdx.x * world + t] = c[t];
+}
+
+// One block: counts[b][d] -> global output offset of block b's rows for d
+// (destination-major, then block order); totals[d] = rows for rank d.
+__global__ __launch_bounds__(kThreads) void k_shard_scan(unsigned long long* __restrict__ counts, int64_t nblocks,
+                                                         int world, unsigned long long* __restrict__ totals) {
+  __shared__ unsigned long long s_tmp[4];
+  const int t = threadIdx.x;
+  const int64_t per = (nblocks + kThreads - 1) / kThreads;
+  const int64_t b0 = (int64_t)t * per;
+  unsigned long long run0 = 0;
+  for (int d = 0; d < world; ++d) {
+    unsigned long long s = 0;
+    for (int64_t b = b0; b < b0 + per && b < nblocks; ++b) s += counts[(size_t)b * world + d];
+    unsigned long long total;
+    unsigned long long run = run0 + block_excl_scan(s, s_tmp, total);
+    for (int64_t b = b0; b < b0 + per && b < nblocks; ++b) {
+      const unsigned long long v = counts[(size_t)b * world + d];
+      counts[(size_t)b * world + d] = run;
+      run += v;
+    }
+    if (t == 0) totals[d] = total;
+    run0 += total;
+  }
+}
+
+__global__ __launch_bounds__(kThreads) void k_shard_scatter(const int64_t* __restrict__ pid,
+                                                            const int64_t* __restrict__ pk,
+                                                            const double* __restrict__ val, int64_t n, int world,
+                                                            const unsigned long long* __restrict__ offsets,
+                                                            int64_t* __restrict__ opid, int64_t* __restrict__ opk,
+                                                            double* __restrict__ oval) {
+  __shared__ unsigned long long base[kShardMax];
+  __shared__ unsigned int wcnt[4][kShardMax];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  if (t < world) base[t] = offsets[(size_t)blockIdx.x * world + t];
+  if (t < kShardMax) wcnt[0][t] = wcnt[1][t] = wcnt[2][t] = wcnt[3][t] = 0;
+  __syncthreads();
+  const int64_t lo = (int64_t)blockIdx.x * kShardChunk;
+  const int64_t hi = lo + kShardChunk < n ? lo + kShardChunk : n;
+  const int dbits = pdp::ceil_log2_u64((uint64_t)world);
+  const uint64_t lt = (1ull << lane) - 1ull;
+  for (int64_t b0 = lo; b0 < hi; b0 += kThreads) {
+    const int64_t i = b0 + t;
+    const bool valid = i < hi;
+    int64_t a = 0, k = 0;
+    double v = 0.0;
+    uint32_t d = 0;
+    if (valid) {
+      a = pid[i];
+      k = pk[i];
+      if (val) v = val[i];
+      d = shard_dest(a, world);
+    }
+    // stable rank among the wave's rows with the same destination
+    uint64_t peers = __ballot(valid);
+    if (!valid) peers = ~peers;
+    for (int bit = 0; bit < dbits; ++bit) {
+      const bool x = (d >> bit) & 1u;
+      const uint64_t bb = __ballot(x);
+      peers &= x ? bb : ~bb;
+    }
+    const uint32_t before = (uint32_t)__popcll(peers & lt);
+    if (valid && before == 0) wcnt[wave][d] = (unsigned int)__popcll(peers);
+    __syncthreads();
+    if (valid) {
+      unsigned long long o = base[d] + before;
+      for (int w = 0; w < wave; ++w) o += wcnt[w][d];
+      opid[o] = a;
+      opk[o] = k;
+      if (val) oval[o] = v;
+    }
+    __syncthreads();
+    if (t < world) {
+      base[t] += (unsigned long long)wcnt[0][t] + wcnt[1][t] + wcnt[2][t] + wcnt[3][t];
+      wcnt[0][t] = wcnt[1][t] = wcnt[2][t] = wcnt[3][t] = 0;
+    }
+    __syncthreads();
   }
 }
 
@@ -1164,6 +1272,38 @@ struct pdp_ctx {
 
 namespace {
 
+// Makes the context's device current for the duration of an entry point and
+// restores the caller's device afterwards (HipBackend(device=k) while another
+// device is current).
+struct DeviceGuard {
+  int prev = -1;
+  bool ok = true;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) ok = hipSetDevice(dev) == hipSuccess;
+  }
+  ~DeviceGuard() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
+// Stream-ordered frees of the generic path's scratch at scope exit, on every
+// return path (HIP_TRY returns early).
+struct AsyncFrees {
+  hipStream_t stream;
+  std::vector<void*> ptrs;
+  explicit AsyncFrees(hipStream_t s) : stream(s) {}
+  hipError_t alloc(void** p, size_t bytes) {
+    const hipError_t e = hipMallocAsync(p, bytes, stream);
+    if (e == hipSuccess) ptrs.push_back(*p);
+    return e;
+  }
+  ~AsyncFrees() {
+    for (void* p : ptrs) (void)hipFreeAsync(p, stream);
+  }
+};
+
 hipEvent_t prof_event(pdp_ctx* ctx) {
   if (!ctx->pool.empty()) {
     hipEvent_t e = ctx->pool.back();
@@ -1209,8 +1349,9 @@ int next_epoch(pdp_ctx* ctx, hipStream_t stream, unsigned long long* status, siz
 int scan_inplace(long long* a, int64_t n, hipStream_t stream) {
   if (n <= 0) return 0;
   const int64_t nb = (n + 2047) / 2048;
+  AsyncFrees scratch(stream);
   long long* sums = nullptr;
-  HIP_TRY(hipMallocAsync((void**)&sums, (size_t)nb * sizeof(long long), stream));
+  HIP_TRY(scratch.alloc((void**)&sums, (size_t)nb * sizeof(long long)));
   hipLaunchKernelGGL(k_scan_chunks, dim3((unsigned)nb), dim3(kThreads), 0, stream, a, n, sums);
   if (nb > 1) {
     int rc = scan_inplace(sums, nb, stream);
@@ -1218,7 +1359,6 @@ int scan_inplace(long long* a, int64_t n, hipStream_t stream) {
     hipLaunchKernelGGL(k_scan_add, dim3((unsigned)nb), dim3(kThreads), 0, stream, a, n, sums);
   }
   HIP_TRY(hipGetLastError());
-  HIP_TRY(hipFreeAsync(sums, stream));
   return 0;
 }
 
@@ -1344,16 +1484,15 @@ int run_generic(pdp_ctx* ctx, const Rec* sorted, Rec* spare, Rec* alt, const std
   ctx->stats.fallback_rows = total;
   ctx->stats.fallback_ranges = nr;
   if (total == 0) return 0;
+  AsyncFrees scratch(stream);
   long long *d_rsrc = nullptr, *d_rdst = nullptr;
-  HIP_TRY(hipMallocAsync((void**)&d_rsrc, nr * sizeof(long long), stream));
-  HIP_TRY(hipMallocAsync((void**)&d_rdst, nr * sizeof(long long), stream));
+  HIP_TRY(scratch.alloc((void**)&d_rsrc, nr * sizeof(long long)));
+  HIP_TRY(scratch.alloc((void**)&d_rdst, nr * sizeof(long long)));
   HIP_TRY(hipMemcpyAsync(d_rsrc, rsrc.data(), nr * sizeof(long long), hipMemcpyHostToDevice, stream));
   HIP_TRY(hipMemcpyAsync(d_rdst, rdst.data(), nr * sizeof(long long), hipMemcpyHostToDevice, stream));
   hipLaunchKernelGGL(k_gather_ranges, dim3(grid_for(total, kThreads)), dim3(kThreads), 0, stream, sorted, spare,
                      d_rsrc, d_rdst, nr, total);
   HIP_TRY(hipStreamSynchronize(stream));  // host vectors go out of scope
-  HIP_TRY(hipFreeAsync(d_rsrc, stream));
-  HIP_TRY(hipFreeAsync(d_rdst, stream));
 
   // 1) rows by (pid, pk), stable (input order within a group)
   Rec* r = nullptr;
@@ -1364,10 +1503,10 @@ int run_generic(pdp_ctx* ctx, const Rec* sorted, Rec* spare, Rec* alt, const std
 
   const size_t m8 = (size_t)total * 8;
   long long *gsc, *psc, *gpos, *pfirst;
-  HIP_TRY(hipMallocAsync((void**)&gsc, m8, stream));
-  HIP_TRY(hipMallocAsync((void**)&psc, m8, stream));
-  HIP_TRY(hipMallocAsync((void**)&gpos, m8 + 8, stream));
-  HIP_TRY(hipMallocAsync((void**)&pfirst, m8, stream));
+  HIP_TRY(scratch.alloc((void**)&gsc, m8));
+  HIP_TRY(scratch.alloc((void**)&psc, m8));
+  HIP_TRY(scratch.alloc((void**)&gpos, m8 + 8));
+  HIP_TRY(scratch.alloc((void**)&pfirst, m8));
   const int gr = grid_for(total, kThreads);
   hipLaunchKernelGGL(k_stream_flags, dim3(gr), dim3(kThreads), 0, stream, r, total, gsc, psc);
   if ((rc = scan_inplace(gsc, total, stream))) return rc;
@@ -1380,12 +1519,12 @@ int run_generic(pdp_ctx* ctx, const Rec* sorted, Rec* spare, Rec* alt, const std
 
   // 2) L_inf ranks: sort (group, row priority, row) -> rank within group.
   Rec *x1, *x2;
-  HIP_TRY(hipMallocAsync((void**)&x1, (size_t)total * sizeof(Rec), stream));
-  HIP_TRY(hipMallocAsync((void**)&x2, (size_t)total * sizeof(Rec), stream));
+  HIP_TRY(scratch.alloc((void**)&x1, (size_t)total * sizeof(Rec)));
+  HIP_TRY(scratch.alloc((void**)&x2, (size_t)total * sizeof(Rec)));
   uint8_t* row_keep;
   int32_t* grank;
-  HIP_TRY(hipMallocAsync((void**)&row_keep, (size_t)total, stream));
-  HIP_TRY(hipMallocAsync((void**)&grank, (size_t)ngroups * 4, stream));
+  HIP_TRY(scratch.alloc((void**)&row_keep, (size_t)total));
+  HIP_TRY(scratch.alloc((void**)&grank, (size_t)ngroups * 4));
   hipLaunchKernelGGL(k_stream_row_prio, dim3(gr), dim3(kThreads), 0, stream, r, total, gsc, gpos, sp.seed, x1);
   Rec* xs = nullptr;
   const int gbits = std::max(1, pdp::ceil_log2_u64((uint64_t)ngroups));
@@ -1407,9 +1546,9 @@ int run_generic(pdp_ctx* ctx, const Rec* sorted, Rec* spare, Rec* alt, const std
   // 4) accumulate kept rows per group, emit kept groups.
   unsigned long long* gcnt;
   double *gx, *gy;
-  HIP_TRY(hipMallocAsync((void**)&gcnt, (size_t)ngroups * 8, stream));
-  HIP_TRY(hipMallocAsync((void**)&gx, (size_t)ngroups * 8, stream));
-  HIP_TRY(hipMallocAsync((void**)&gy, (size_t)ngroups * 8, stream));
+  HIP_TRY(scratch.alloc((void**)&gcnt, (size_t)ngroups * 8));
+  HIP_TRY(scratch.alloc((void**)&gx, (size_t)ngroups * 8));
+  HIP_TRY(scratch.alloc((void**)&gy, (size_t)ngroups * 8));
   HIP_TRY(hipMemsetAsync(gcnt, 0, (size_t)ngroups * 8, stream));
   HIP_TRY(hipMemsetAsync(gx, 0, (size_t)ngroups * 8, stream));
   HIP_TRY(hipMemsetAsync(gy, 0, (size_t)ngroups * 8, stream));
@@ -1419,9 +1558,6 @@ int run_generic(pdp_ctx* ctx, const Rec* sorted, Rec* spare, Rec* alt, const std
                      gcnt, gx, gy, acc);
   HIP_TRY(hipGetLastError());
   (void)r_other;
-  for (void* p : {(void*)gsc, (void*)psc, (void*)gpos, (void*)pfirst, (void*)x1, (void*)x2, (void*)row_keep,
-                  (void*)grank, (void*)gcnt, (void*)gx, (void*)gy})
-    HIP_TRY(hipFreeAsync(p, stream));
   return 0;
 }
 
@@ -1459,6 +1595,18 @@ double norm_ppf(double p) {
   const double e = std_normal_cdf(x) - p;
   const double u = e * std::sqrt(2 * M_PI) * std::exp(x * x / 2);
   return x - u / (1 + x * u / 2);
+}
+
+// Per-partition delta of a selection strategy over k = max_partitions_contributed
+// partitions: 1 - (1 - delta)^(1/k), so that k independent per-partition
+// decisions compose to delta; eps is split as eps / k.  One adjustment for all
+// three strategies (truncated geometric, Laplace and Gaussian thresholding).
+// PyDP's (partition_selection.py:24-33) is parity unpinned for k > 1: the
+// reference pins only k = 1 (analysis/tests/combiners_test.py:197-224), where
+// this is delta.  It differs from delta / k by less than delta^2 / 2.
+double adjusted_delta(double delta, int64_t k) {
+  if (k <= 1) return delta;
+  return -std::expm1(std::log1p(-delta) / (double)k);
 }
 
 double noise_scale(int kind, double eps, double delta, double l0, double linf) {
@@ -1531,7 +1679,7 @@ double pdp_gaussian_sigma(double eps, double delta, double l2) {
 
 int pdp_truncated_geometric_table(double eps, double delta, int64_t k, double* out, int64_t cap, int64_t* length) {
   if (!(eps > 0) || delta < 0 || k <= 0 || !length) return fail(PDP_ERR_INVALID_ARG, "bad truncated geometric args");
-  const double e = eps / (double)k, d = delta / (double)k;
+  const double e = eps / (double)k, d = adjusted_delta(delta, k);
   const double ee = std::exp(e), eme = std::exp(-e);
   double prev = 0.0;
   int64_t len = 1;
@@ -1551,7 +1699,7 @@ int pdp_truncated_geometric_table(double eps, double delta, int64_t k, double* o
 int pdp_selection_threshold(int32_t selection, double eps, double delta, int64_t k, double* thr, double* scale) {
   if (!(eps > 0) || k <= 0) return fail(PDP_ERR_INVALID_ARG, "bad selection args");
   if (selection == PDP_SELECTION_LAPLACE_THRESHOLDING) {
-    const double adj = 1.0 - std::pow(1.0 - delta, 1.0 / (double)k);
+    const double adj = adjusted_delta(delta, k);
     const double b = (double)k / eps;
     *scale = b;
     *thr = adj > 0.5 ? 1.0 + b * std::log(2.0 * (1.0 - adj)) : 1.0 - b * std::log(2.0 * adj);
@@ -1561,7 +1709,7 @@ int pdp_selection_threshold(int32_t selection, double eps, double delta, int64_t
     if (!(delta > 0)) return fail(PDP_ERR_INVALID_ARG, "Gaussian thresholding needs delta > 0");
     const double td = delta / 2.0, nd = delta - td;
     const double sigma = pdp_gaussian_sigma(eps, nd, std::sqrt((double)k));
-    const double adj = 1.0 - std::pow(1.0 - td, 1.0 / (double)k);
+    const double adj = adjusted_delta(td, k);
     *scale = sigma;
     *thr = 1.0 + sigma * norm_ppf(1.0 - adj);
     return 0;
@@ -1599,6 +1747,8 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
                const pdp_accumulators* accps, void* workspace, size_t workspace_bytes, void* stream_, bool sweep) {
   if (!ctx || !cols || !bps || !accps) return fail(PDP_ERR_INVALID_ARG, "null argument");
   if (nconf < 1) return fail(PDP_ERR_INVALID_ARG, "num_configs must be >= 1");
+  DeviceGuard dg(ctx->device);
+  if (!dg.ok) return fail(PDP_ERR_HIP, "hipSetDevice failed");
   hipStream_t stream = (hipStream_t)stream_;
   const pdp_bound_params* bp = &bps[0];
   const int64_t n = cols->num_rows, U = cols->num_privacy_ids, P = cols->num_partitions;
@@ -1826,6 +1976,8 @@ int pdp_release(pdp_ctx* ctx, const pdp_accumulators* accp, int64_t P, int64_t p
                 const pdp_release_params* rp, const pdp_outputs* out, void* stream_) {
   if (!ctx || !accp || !rp || !out || !out->keep || !out->metrics) return fail(PDP_ERR_INVALID_ARG, "null argument");
   if (P < 0) return fail(PDP_ERR_INVALID_ARG, "num_partitions < 0");
+  DeviceGuard dg(ctx->device);
+  if (!dg.ok) return fail(PDP_ERR_HIP, "hipSetDevice failed");
   hipStream_t stream = (hipStream_t)stream_;
   RelParams q{};
   q.metrics = rp->metrics;
@@ -1977,6 +2129,48 @@ int pdp_profile_read(pdp_ctx* ctx, double* ms_out, int64_t* launches_out, int re
       ctx->prof_n[i] = 0;
     }
   }
+  return 0;
+}
+
+int pdp_shard_workspace_size(int64_t num_rows, int32_t world_size, size_t* bytes) {
+  if (!bytes || num_rows < 0 || world_size < 1 || world_size > kShardMax)
+    return fail(PDP_ERR_INVALID_ARG, "bad shard workspace args");
+  const int64_t nb = std::max<int64_t>(1, (num_rows + kShardChunk - 1) / kShardChunk);
+  *bytes = align_up((size_t)nb * world_size * 8, 256) + align_up((size_t)kShardMax * 8, 256);
+  return 0;
+}
+
+int pdp_shard_rows(pdp_ctx* ctx, const pdp_columns* cols, int32_t world_size, int64_t* out_pid, int64_t* out_pk,
+                   double* out_value, int64_t* rows_per_rank, void* workspace, size_t workspace_bytes,
+                   void* stream_) {
+  if (!ctx || !cols || !rows_per_rank) return fail(PDP_ERR_INVALID_ARG, "null argument");
+  if (world_size < 1 || world_size > kShardMax) return fail(PDP_ERR_INVALID_ARG, "world_size must be in [1, 64]");
+  const int64_t n = cols->num_rows;
+  if (n < 0) return fail(PDP_ERR_INVALID_ARG, "num_rows < 0");
+  for (int d = 0; d < world_size; ++d) rows_per_rank[d] = 0;
+  if (n == 0) return 0;
+  if (!cols->pid || !cols->pk || !out_pid || !out_pk) return fail(PDP_ERR_INVALID_ARG, "pid / pk columns required");
+  if ((cols->value == nullptr) != (out_value == nullptr))
+    return fail(PDP_ERR_INVALID_ARG, "value and out_value must both be set or both be null");
+  size_t need = 0;
+  if (int rc = pdp_shard_workspace_size(n, world_size, &need)) return rc;
+  if (!workspace || workspace_bytes < need) return fail(PDP_ERR_WORKSPACE, "workspace too small");
+  DeviceGuard dg(ctx->device);
+  if (!dg.ok) return fail(PDP_ERR_HIP, "hipSetDevice failed");
+  hipStream_t stream = (hipStream_t)stream_;
+  const int64_t nb = (n + kShardChunk - 1) / kShardChunk;
+  unsigned long long* counts = (unsigned long long*)workspace;
+  unsigned long long* totals = (unsigned long long*)((char*)workspace + align_up((size_t)nb * world_size * 8, 256));
+  hipLaunchKernelGGL(k_shard_count, dim3((unsigned)nb), dim3(kThreads), 0, stream, cols->pid, n, (int)world_size,
+                     counts);
+  hipLaunchKernelGGL(k_shard_scan, dim3(1), dim3(kThreads), 0, stream, counts, nb, (int)world_size, totals);
+  hipLaunchKernelGGL(k_shard_scatter, dim3((unsigned)nb), dim3(kThreads), 0, stream, cols->pid, cols->pk,
+                     cols->value, n, (int)world_size, (const unsigned long long*)counts, out_pid, out_pk, out_value);
+  HIP_TRY(hipGetLastError());
+  unsigned long long host[kShardMax];
+  HIP_TRY(hipMemcpyAsync(host, totals, (size_t)world_size * 8, hipMemcpyDeviceToHost, stream));
+  HIP_TRY(hipStreamSynchronize(stream));
+  for (int d = 0; d < world_size; ++d) rows_per_rank[d] = (int64_t)host[d];
   return 0;
 }
 

@@ -8,10 +8,11 @@
 //     /root/reference/pipeline_dp/pipeline_backend.py:504-520);
 //   * a keyed Feistel bijection (only used to scramble Zipf ranks in the
 //     synthetic generator);
-//   * Philox4x32-10 (Random123) -> uniform doubles in (0,1) -> Laplace by
-//     inverse CDF, Gaussian by Box-Muller.
-// The noise is Philox-based and is NOT PyDP's secure (granularity-rounded)
-// noise; see DESIGN.md.
+//   * Philox4x32-10 (Random123) -> uniforms in (0,1) -> Laplace as a
+//     two-sided geometric on a power-of-two grid, Gaussian by Box-Muller
+//     rounded to that grid; released values are snapped to the grid too.
+// The noise is Philox-based: granularity-snapped like PyDP's secure
+// mechanisms, but not PyDP's implementation; see DESIGN.md.
 #pragma once
 #include <stdint.h>
 #include <math.h>
@@ -146,18 +147,52 @@ PDP_HD void philox_uniforms(uint64_t seed, uint64_t idx, uint32_t stream, double
   u2 = uniform53(r.z, r.w);
 }
 
-PDP_HD double unit_laplace(uint64_t seed, uint64_t idx, uint32_t stream) {
-  double u, unused;
-  philox_uniforms(seed, idx, stream, u, unused);
-  const double d = u - 0.5;
-  const double m = log1p(-2.0 * fabs(d));
-  return d > 0.0 ? -m : (d < 0.0 ? m : 0.0);
+// Uniform in (0, 1) from a 64-bit word (hi:lo), with full relative precision
+// near 0: u >= 2^-11 from the top 53 bits, below that exactly (w + 1/2) 2^-64.
+// -log(u) then reaches 45 instead of the 36.7 of a 53-bit uniform, so the
+// noise tails are not cut at 36.7 scales.
+PDP_HD double uniform64(uint32_t hi, uint32_t lo) {
+  const uint64_t w = ((uint64_t)hi << 32) | lo;
+  if (w >= (1ull << 53)) return ((double)(w >> 11) + 0.5) * (1.0 / 9007199254740992.0);
+  return ((double)w + 0.5) * 5.421010862427522e-20;  // 2^-64
 }
 
-PDP_HD double unit_gaussian(uint64_t seed, uint64_t idx, uint32_t stream) {
-  double u1, u2;
-  philox_uniforms(seed, idx, stream, u1, u2);
-  return sqrt(-2.0 * log(u1)) * cos(6.283185307179586 * u2);
+// Noise grid of a mechanism with scale s (Laplace b or Gaussian sigma):
+// g = 2^(ceil(log2 s) - 40).  Released values are multiples of g (the
+// granularity snapping of PyDP's secure mechanisms, against the
+// floating-point attack on textbook Laplace; the grid is 2^-40 of the scale,
+// invisible to every distributional test).
+PDP_HD double noise_grid(double s) {
+  int e = 0;
+  const double m = frexp(s, &e);
+  return ldexp(1.0, (m == 0.5 ? e - 1 : e) - 40);
+}
+
+// Laplace(0, b) on the grid g: g * (G1 - G2) with G_i = floor(E_i b / g),
+// E_i ~ Exp(1) from the two 64-bit Philox words -- the two-sided geometric
+// distribution P(k g) ~ exp(-|k| g / b).
+PDP_HD double laplace_on_grid(uint64_t seed, uint64_t idx, uint32_t stream, double b, double g) {
+  u32x4 c{(uint32_t)idx, (uint32_t)(idx >> 32), stream, 0u};
+  const u32x4 r = philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+  const double e1 = -log(uniform64(r.x, r.y)), e2 = -log(uniform64(r.z, r.w));
+  return g * (floor(e1 * (b / g)) - floor(e2 * (b / g)));
+}
+
+// N(0, sigma^2) by Box-Muller, rounded to the grid g.
+PDP_HD double gaussian_on_grid(uint64_t seed, uint64_t idx, uint32_t stream, double sigma, double g) {
+  u32x4 c{(uint32_t)idx, (uint32_t)(idx >> 32), stream, 0u};
+  const u32x4 r = philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+  const double z = sqrt(-2.0 * log(uniform64(r.x, r.y))) * cos(6.283185307179586 * uniform53(r.z, r.w));
+  return g * rint(sigma * z / g);
+}
+
+// value + noise with both on the grid of `scale` (kind 0 Laplace, 1 Gaussian).
+PDP_HD double add_snapped_noise(int gaussian, double value, uint64_t seed, uint64_t idx, uint32_t stream,
+                                double scale) {
+  const double g = noise_grid(scale);
+  const double z = gaussian ? gaussian_on_grid(seed, idx, stream, scale, g)
+                            : laplace_on_grid(seed, idx, stream, scale, g);
+  return g * rint(value / g) + z;
 }
 
 }  // namespace pdp

@@ -53,6 +53,42 @@ class World:
         off = min(self.rank * b, num_partitions)
         return off, max(0, min(b, num_partitions - off)), b * self.size
 
+    def check_same(self, value: int, what: str, device=None):
+        """All ranks must agree on `value` (e.g. the number of partitions of
+        the dense key space they reduce-scatter); raises otherwise."""
+        import torch
+        import torch.distributed as dist
+        t = torch.tensor([int(value), -int(value)], dtype=torch.int64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+        if int(t[0]) != -int(t[1]):
+            raise ValueError(f"ranks disagree on {what}: {int(value)} here, range [{-int(t[1])}, {int(t[0])}]")
+
+    def shuffle_by_privacy_id(self, ex, pid, pk, value):
+        """Moves every row to rank shard_of(pid): pdp_shard_rows groups the
+        local rows by destination (stable), then one all-to-all per column
+        (RCCL over xGMI on GPUs).  Rank r receives rank 0's rows for it first,
+        then rank 1's, ...: the input order of the concatenated ranks is kept
+        within every privacy id, so the bounding result equals one process
+        over the concatenated input (the reference's group-by-pid shuffle,
+        pipeline_backend.py:261,401,476-485)."""
+        import torch
+        import torch.distributed as dist
+        spid, spk, sval, counts = ex.shard_rows(pid, pk, value, self.size)
+        send = torch.tensor(counts, dtype=torch.int64, device=pk.device)
+        recv = torch.empty_like(send)
+        dist.all_to_all_single(recv, send, group=self.group)
+        out_splits = [int(x) for x in recv.tolist()]
+        total = sum(out_splits)
+
+        def move(t):
+            if t is None:
+                return None
+            out = t.new_empty(total)
+            dist.all_to_all_single(out, t.contiguous(), out_splits, counts, group=self.group)
+            return out
+
+        return move(spid), move(spk), move(sval)
+
     def reduce_scatter_accumulators(self, acc, num_partitions: int):
         """Sums per-rank dense accumulators; returns owned-block tensors
         [row_count, count, x, y] (None where absent)."""
@@ -73,14 +109,18 @@ class World:
             outs.append(dst)
         return outs
 
-    def aggregate(self, ex, pid, pk, value, num_privacy_ids, num_partitions, bounds, rel, gather=True):
+    def aggregate(self, ex, pid, pk, value, num_privacy_ids, num_partitions, bounds, rel, gather=True,
+                  shuffle=False):
         """Rank-local bound+accumulate, reduce-scatter, owner-side release.
 
-        Returns (keep [P], metrics [F, P], fields) of ALL partitions on every
-        rank when ``gather`` (all-gather of the owned blocks), else of the
-        owned block only."""
-        import torch
+        ``shuffle``: first move every row to rank shard_of(pid)
+        (``shuffle_by_privacy_id``); without it the rows must already be
+        sharded by privacy id.  Returns (keep [P], metrics [F, P], fields) of
+        ALL partitions on every rank when ``gather`` (all-gather of the owned
+        blocks), else of the owned block only."""
         import torch.distributed as dist
+        if shuffle and pid is not None:
+            pid, pk, value = self.shuffle_by_privacy_id(ex, pid, pk, value)
         acc = ex.accumulate(pid, pk, value, num_privacy_ids, num_partitions, bounds)
         off, length, padded = self.block(num_partitions)
         owned = self.reduce_scatter_accumulators(acc, num_partitions)

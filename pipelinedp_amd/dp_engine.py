@@ -118,15 +118,28 @@ class DPResult:
         return ReleaseConfig(mask, noise_kind, selection, eps, delta, self._plan.max_rows_per_privacy_id,
                              add_noise=not self._backend._disable_noise, noise_seed=self._backend.noise_seed)
 
-    def _inputs(self, torch, device, need_pid, need_value):
+    def _inputs(self, torch, device, need_pid, need_value, world=None):
         """-> pid, pk, value device tensors, U, P, partition keys."""
         col = self._col
         public = self._public
+        multi = world is not None and world.size > 1
+
+        def global_max(t, local):
+            # multi-rank: the id ranges are the union over ranks
+            if not multi:
+                return local
+            import torch.distributed as dist
+            m = torch.tensor([local], dtype=torch.int64, device=device)
+            dist.all_reduce(m, op=dist.ReduceOp.MAX, group=world.group)
+            return int(m.item())
+
         if isinstance(col, ColumnarData):
             pk = torch.as_tensor(col.partition).to(device=device, dtype=torch.int64).contiguous()
             P = col.num_partitions
             if P is None:
-                P = int(pk.max().item()) + 1 if pk.numel() else 0
+                P = global_max(pk, int(pk.max().item()) + 1 if pk.numel() else 0)
+            elif pk.numel() and int(pk.max().item()) >= P:
+                raise ValueError(f"partition id {int(pk.max().item())} >= num_partitions={P}")
             keys = list(col.partition_keys) if col.partition_keys is not None else list(range(P))
             if public is not None:
                 lut, keys = remap_public(pk, col.partition_keys, P, public)
@@ -139,12 +152,12 @@ class DPResult:
                 pid = torch.as_tensor(col.privacy_id).to(device=device, dtype=torch.int64).contiguous()
                 U = col.num_privacy_ids
                 if U is None:
-                    U = int(pid.max().item()) + 1 if pid.numel() else 1
+                    U = global_max(pid, int(pid.max().item()) + 1 if pid.numel() else 1)
             value = None
             if need_value:
                 value = torch.as_tensor(col.value).to(device=device, dtype=torch.float64).contiguous()
             return pid, pk, value, U, P, keys
-        enc = encode_rows(col, self._extractors, public, need_pid=need_pid, need_value=need_value)
+        enc = encode_rows(col, self._extractors, public, need_pid=need_pid, need_value=need_value, world=world)
         t = lambda a: torch.from_numpy(a).to(device)  # noqa: E731
         return (t(enc.pid) if enc.pid is not None else None, t(enc.pk),
                 t(enc.value) if enc.value is not None else None, enc.num_privacy_ids, len(enc.partition_keys),
@@ -167,9 +180,15 @@ class DPResult:
                                  enforced, backend.sampling_seed, backend._debug_force_fallback)
         rel = self._release_config(mask)  # raises before any work if budgets are not computed
         need_value = bool(mask & (native.METRIC_SUM | native.METRIC_MEAN | native.METRIC_VARIANCE))
-        pid, pk, value, U, P, keys = self._inputs(torch, ex.device, not enforced, need_value)
-        if backend.world is not None and backend.world.size > 1:
-            keep, out, fields = backend.world.aggregate(ex, pid, pk, value, U, P, bounds, rel)
+        world = backend.world if backend.world is not None and backend.world.size > 1 else None
+        pid, pk, value, U, P, keys = self._inputs(torch, ex.device, not enforced, need_value, world)
+        fields = native.metric_fields(mask)
+        if P == 0:  # e.g. public_partitions=[]: nothing to release (reference: empty collection)
+            return keys, np.zeros(0, dtype=bool), fields, np.zeros((len(fields), 0))
+        if world is not None:
+            world.check_same(P, "num_partitions", pk.device)
+            presharded = isinstance(self._col, ColumnarData) and self._col.privacy_id_sharded
+            keep, out, fields = world.aggregate(ex, pid, pk, value, U, P, bounds, rel, shuffle=not presharded)
         else:
             acc = ex.accumulate(pid, pk, value, U, P, bounds)
             keep, out, fields = ex.release(acc, rel, bounds)

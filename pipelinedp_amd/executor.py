@@ -185,6 +185,25 @@ class HipExecutor:
                                           ctypes.byref(outs), self.stream_handle), "pdp_release")
         return keep[:P], out[:, :P], fields
 
+    def shard_rows(self, pid, pk, value, world_size: int):
+        """pdp_shard_rows: rows grouped by destination rank shard_of(pid)
+        (stable) -> (pid, pk, value, rows_per_rank list)."""
+        torch = self.torch
+        n = int(pk.numel())
+        cols = self._columns(pid, pk, value, 1, 1)
+        opid = torch.empty(max(n, 1), dtype=torch.int64, device=self.device)[:n]
+        opk = torch.empty(max(n, 1), dtype=torch.int64, device=self.device)[:n]
+        oval = torch.empty(max(n, 1), dtype=torch.float64, device=self.device)[:n] if value is not None else None
+        nbytes = ctypes.c_size_t(0)
+        native.check(self.lib.pdp_shard_workspace_size(n, int(world_size), ctypes.byref(nbytes)),
+                     "pdp_shard_workspace_size")
+        ws = torch.empty(max(nbytes.value, 256), dtype=torch.uint8, device=self.device)
+        counts = (ctypes.c_int64 * int(world_size))()
+        native.check(self.lib.pdp_shard_rows(self.ctx, ctypes.byref(cols), int(world_size), _ptr(opid), _ptr(opk),
+                                             _ptr(oval), counts, ctypes.c_void_p(ws.data_ptr()), ws.numel(),
+                                             self.stream_handle), "pdp_shard_rows")
+        return opid, opk, oval, list(counts)
+
     def profile(self, enable: bool = True):
         native.check(self.lib.pdp_profile_enable(self.ctx, int(enable)), "pdp_profile_enable")
 

@@ -81,6 +81,9 @@ SIGNATURES = [
                                               ctypes.POINTER(c_i64)]),
     ("pdp_selection_threshold", c_i32, [c_i32, c_f64, c_f64, c_i64, ctypes.POINTER(c_f64),
                                         ctypes.POINTER(c_f64)]),
+    ("pdp_shard_workspace_size", c_i32, [c_i64, c_i32, ctypes.POINTER(ctypes.c_size_t)]),
+    ("pdp_shard_rows", c_i32, [c_vp, ctypes.POINTER(Columns), c_i32, c_vp, c_vp, c_vp, ctypes.POINTER(c_i64), c_vp,
+                               ctypes.c_size_t, c_vp]),
     ("pdp_generate_synthetic", c_i32, [c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_f64, c_i32, c_f64,
                                        c_f64, c_u64, c_vp]),
     ("pdp_get_stats", c_i32, [c_vp, ctypes.POINTER(Stats)]),

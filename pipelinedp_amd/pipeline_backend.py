@@ -5,9 +5,9 @@
 same seam.  ``HipBackend`` is the new MI355X plugin: it advertises the fused
 columnar aggregate capability that ``DPEngine.aggregate`` dispatches to.  Its
 per-element collection ops are host plumbing for post-processing results
-(e.g. ``make_private(...).mean`` extracting ``.mean``); the per-key sampling
-and combining ops that make up the hot path are not offered element-wise —
-they run fused on the GPU.
+(e.g. ``make_private(...).mean`` extracting ``.mean``) and the complete
+element-wise op set of the reference ABC on the host; the hot path itself
+(bounding + combining + selection + noise) runs fused on the GPU.
 """
 import abc
 import collections
@@ -200,11 +200,28 @@ class HipBackend(PipelineBackend):
     def to_list(self, col, stage_name=None):
         return iter([list(col)])
 
-    # -- hot-path ops: fused on the GPU, not offered element-wise ------------
+    # -- per-key sampling / combining, element-wise on the host ---------------
+    # DPEngine.aggregate / select_partitions never call these: bounding and
+    # combining run fused on the GPU.  They complete the PipelineBackend seam
+    # (the reference's 17 abstract ops) for callers that build their own
+    # element-wise graphs, with LocalBackend's semantics.
     def sample_fixed_per_key(self, col, n, stage_name=None):
-        raise NotImplementedError("HipBackend fuses contribution bounding into DPEngine.aggregate on the GPU; "
-                                  "element-wise sample_fixed_per_key is not offered.")
+        """Per key, a uniform sample of <= n values without replacement
+        (LocalBackend.sample_fixed_per_key, pipeline_backend.py:504-520)."""
+        import numpy as np
+
+        def gen():
+            rng = np.random.default_rng(self.sampling_seed)
+            for key, values in self.group_by_key(col):
+                if len(values) > n:
+                    idx = rng.choice(len(values), n, replace=False)
+                    values = [values[i] for i in idx]
+                yield key, values
+
+        return gen()
 
     def combine_accumulators_per_key(self, col, combiner, stage_name=None):
-        raise NotImplementedError("HipBackend fuses per-partition combining into DPEngine.aggregate on the GPU; "
-                                  "element-wise combine_accumulators_per_key is not offered.")
+        """Per key, the accumulators merged with combiner.merge_accumulators
+        (LocalBackend.combine_accumulators_per_key, pipeline_backend.py:528-538)."""
+        return self.map_values(self.group_by_key(col),
+                               lambda accs: functools.reduce(combiner.merge_accumulators, accs))

@@ -1,0 +1,86 @@
+"""CPU stand-in for ``pipelinedp_amd.executor.HipExecutor`` -- TEST
+INFRASTRUCTURE ONLY.
+
+Implements the executor interface (accumulate / release / shard_rows) on CPU
+torch tensors with the numpy oracle, so that the host logic around the HIP
+library -- DPEngine's lazy result, the multi-rank dictionary agreement, the
+privacy-id shuffle, reduce-scatter and owner-side release of
+``pipelinedp_amd/distributed.py`` -- can run under gloo in the CPU suite.
+The product never imports this: HipBackend builds a HipExecutor, which
+fails loudly without a GPU; tests inject this object instead.
+"""
+import numpy as np
+
+import pdp_oracle as o
+from pipelinedp_amd import native
+
+_NAMES = ((native.METRIC_VARIANCE, "variance"), (native.METRIC_MEAN, "mean"), (native.METRIC_COUNT, "count"),
+          (native.METRIC_SUM, "sum"), (native.METRIC_PRIVACY_ID_COUNT, "privacy_id_count"))
+_SLOTS = {"count": native.MECH_COUNT, "sum": native.MECH_SUM, "mean": native.MECH_MEAN,
+          "variance": native.MECH_VARIANCE, "privacy_id_count": native.MECH_PRIVACY_ID_COUNT}
+_SEL = {native.SELECTION_TRUNCATED_GEOMETRIC: "truncated_geometric", native.SELECTION_LAPLACE: "laplace",
+        native.SELECTION_GAUSSIAN: "gaussian"}
+
+
+def _bound_params(b):
+    return o.BoundParams(b.max_partitions_contributed, b.max_contributions_per_partition, b.min_value, b.max_value,
+                         b.min_sum_per_partition, b.max_sum_per_partition, b.bounds_already_enforced)
+
+
+class _Acc:
+
+    def __init__(self, torch, acc, mask, P):
+        self.num_partitions = P
+        mean_like = mask & (native.METRIC_MEAN | native.METRIC_VARIANCE)
+        self.row_count = torch.from_numpy(acc.row_count.astype(np.int64))
+        self.count = torch.from_numpy(acc.count.astype(np.int64))
+        self.x = torch.from_numpy(np.asarray(acc.nsum if mean_like else acc.sum, np.float64))
+        self.y = torch.from_numpy(np.asarray(acc.nsumsq, np.float64))
+
+
+class CpuExecutor:
+
+    def __init__(self):
+        import torch
+        self.torch = torch
+        self.device = torch.device("cpu")
+        self.calls = []
+
+    def accumulate(self, pid, pk, value, num_privacy_ids, num_partitions, cfg):
+        self.calls.append(("accumulate", int(pk.numel())))
+        acc = o.bound_and_accumulate(None if pid is None else pid.numpy(), pk.numpy(),
+                                     None if value is None else value.numpy(), num_partitions, _bound_params(cfg),
+                                     "hash", seed=cfg.sampling_seed or 0)
+        return _Acc(self.torch, acc, cfg.metrics_mask, num_partitions)
+
+    def release(self, acc, cfg, bounds, pk_offset=0, num_partitions=None):
+        torch = self.torch
+        P = acc.num_partitions if num_partitions is None else int(num_partitions)
+        mask = cfg.metrics_mask
+        names = tuple(n for bit, n in _NAMES if mask & bit)
+        budgets = {n: (cfg.eps[s], cfg.delta[s]) for n, s in _SLOTS.items() if n in names}
+        sel = _SEL.get(cfg.selection)
+        spec = o.ReleaseSpec(names, "gaussian" if cfg.noise_kind == native.NOISE_GAUSSIAN else "laplace", budgets, sel,
+                             (cfg.eps[native.MECH_SELECTION], cfg.delta[native.MECH_SELECTION]),
+                             cfg.max_rows_per_privacy_id)
+        mean_like = mask & (native.METRIC_MEAN | native.METRIC_VARIANCE)
+        x = acc.x.numpy()[:P] if acc.x is not None else np.zeros(P)
+        y = acc.y.numpy()[:P] if acc.y is not None else np.zeros(P)
+        z = np.zeros(P)
+        oacc = o.Accumulators(acc.row_count.numpy()[:P], acc.count.numpy()[:P] if acc.count is not None else z,
+                              z if mean_like else x, x if mean_like else z, y)
+        keep, out = o.release(oacc, _bound_params(bounds), spec, seed=cfg.noise_seed or 0, noise=cfg.add_noise,
+                              pk_idx=np.arange(pk_offset, pk_offset + P))
+        fields = o.metric_field_order(names)
+        metrics = np.stack([out[f] for f in fields]) if fields else np.zeros((1, P))
+        return torch.from_numpy(keep.astype(np.uint8)), torch.from_numpy(metrics), fields
+
+    def shard_rows(self, pid, pk, value, world_size):
+        """pdp_shard_rows restated: stable grouping by shard_of(pid)."""
+        from pipelinedp_amd.distributed import shard_of
+        torch = self.torch
+        dest = shard_of(pid.numpy(), world_size)
+        order = np.argsort(dest, kind="stable")
+        counts = np.bincount(dest, minlength=world_size).tolist()
+        take = lambda t: None if t is None else torch.from_numpy(np.ascontiguousarray(t.numpy()[order]))  # noqa
+        return take(pid), take(pk), take(value), counts

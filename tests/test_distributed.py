@@ -133,3 +133,104 @@ def test_two_ranks_match_single_process(two_rank_run):
     for r in two_rank_run:
         off, ln = int(r["off"]), int(r["length"])
         assert np.array_equal(r["row_count"], acc.row_count[off:off + ln])
+
+
+# --- DPEngine.aggregate with a 2-rank world (gloo) ---------------------------
+# Rows are dealt round-robin (NOT sharded by privacy id) and carry string keys,
+# so the run exercises the cross-rank key dictionaries (columnar._global_keys),
+# the num_partitions agreement, the privacy-id shuffle (World.shuffle_by_privacy_id
+# over all_to_all_single), reduce-scatter and owner-side release.  The HIP
+# executor is replaced by tests/cpu_executor.py (oracle on CPU tensors).
+# Expected: one process over the concatenation [rank 0 rows, rank 1 rows] --
+# the same dense ids, the same privacy-id row order, hence identical sampling
+# and Philox draws: counts / keep decisions exact, fp64 to 1e-9.
+
+
+def _engine_rows():
+    pid, pk, val = o.synth_rows(6000, 300, 40, seed=23, zipf_s=1.1)
+    return [(f"user{a}", f"movie{b}", float(v)) for a, b, v in zip(pid, pk, val)]
+
+
+def _run_engine(rows, world):
+    import pipelinedp_amd as pdp
+    from cpu_executor import CpuExecutor
+    backend = pdp.HipBackend(world=world, sampling_seed=5, noise_seed=9)
+    backend._executor = CpuExecutor()
+    acct = pdp.NaiveBudgetAccountant(total_epsilon=10, total_delta=1e-3)
+    engine = pdp.DPEngine(acct, backend)
+    params = pdp.AggregateParams(metrics=[pdp.Metrics.COUNT, pdp.Metrics.SUM, pdp.Metrics.MEAN,
+                                          pdp.Metrics.PRIVACY_ID_COUNT],
+                                 max_partitions_contributed=3, max_contributions_per_partition=2,
+                                 min_value=0.0, max_value=10.0)
+    ex = pdp.DataExtractors(privacy_id_extractor=lambda r: r[0], partition_extractor=lambda r: r[1],
+                            value_extractor=lambda r: r[2])
+    res = engine.aggregate(rows, params, ex)
+    acct.compute_budgets()
+    return sorted((k, tuple(t)) for k, t in res), list(backend._executor.calls)
+
+
+def _engine_worker(rank, world_size, port, outdir):
+    import json
+
+    import torch.distributed as dist
+
+    from pipelinedp_amd.distributed import World
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world_size)
+    try:
+        rows = _engine_rows()[rank::world_size]
+        out, calls = _run_engine(rows, World(rank, world_size))
+        with open(os.path.join(outdir, f"engine{rank}.json"), "w") as f:
+            json.dump({"out": out, "calls": calls, "rows_in": len(rows)}, f)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.fixture(scope="module")
+def engine_two_ranks(tmp_path_factory):
+    import json
+
+    import torch.multiprocessing as mp
+    outdir = str(tmp_path_factory.mktemp("engine"))
+    mp.spawn(_engine_worker, args=(2, _free_port(), outdir), nprocs=2, join=True)
+    return [json.load(open(os.path.join(outdir, f"engine{r}.json"))) for r in range(2)]
+
+
+def test_dp_engine_two_ranks_matches_one_process(engine_two_ranks):
+    rows = _engine_rows()
+    concat = rows[0::2] + rows[1::2]
+    want, _ = _run_engine(concat, None)
+    assert len(want) > 5
+    for r in engine_two_ranks:
+        got = [(k, tuple(v)) for k, v in r["out"]]
+        assert [k for k, _ in got] == [k for k, _ in want]
+        for (_, g), (_, w) in zip(got, want):
+            np.testing.assert_allclose(g, w, rtol=1e-9, atol=1e-9)
+
+
+def test_dp_engine_two_ranks_shuffle_moves_rows_by_privacy_id(engine_two_ranks):
+    # after the shuffle each rank bounds only its own privacy ids: the rows
+    # each rank accumulates add up to all rows, and differ from what it was given
+    acc_rows = [c[1] for r in engine_two_ranks for c in r["calls"] if c[0] == "accumulate"]
+    assert sum(acc_rows) == len(_engine_rows())
+    assert acc_rows != [r["rows_in"] for r in engine_two_ranks]
+
+
+def test_world_check_same_raises_on_disagreement(tmp_path):
+    import torch.multiprocessing as mp
+    mp.spawn(_disagree_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    assert sorted(os.listdir(tmp_path)) == ["raised0", "raised1"]
+
+
+def _disagree_worker(rank, world_size, port, outdir):
+    import torch.distributed as dist
+
+    from pipelinedp_amd.distributed import World
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world_size)
+    try:
+        World(rank, world_size).check_same(10, "num_partitions")
+        try:
+            World(rank, world_size).check_same(10 + rank, "num_partitions")
+        except ValueError:
+            open(os.path.join(outdir, f"raised{rank}"), "w").close()
+    finally:
+        dist.destroy_process_group()

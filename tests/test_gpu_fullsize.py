@@ -86,3 +86,98 @@ def test_headline_1b_rows_binding_invariants(ex):
     assert torch.equal(acc2.count, cnt)
     absmax = cnt.to(torch.float64) * (b - a) / 2
     assert bool(((acc2.x - nsum).abs() <= 1e-9 * (absmax + 1.0)).all())
+
+
+def test_c3_release_selection_and_noise_full_size(ex):
+    """pdp_release at the headline size (1e9 rows): noise-free means equal
+    nsum / max(1, count) + mid (compute_dp_mean, dp_computations.py:353-397);
+    with noise, the truncated-geometric keep count lies within 5 sigma of
+    sum_p p(n_p) over the observed privacy-id counts (dp_engine.py:312-362)."""
+    import math
+
+    import numpy as np
+    import torch
+
+    import pdp_oracle as o
+    from pipelinedp_amd import native
+    from pipelinedp_amd.executor import BoundConfig, ReleaseConfig
+    n, U, P, L0, Linf, a, b = 1_000_000_000, 10_000_000, 1_000_000, 4, 2, 0.0, 10.0
+    pid, pk, val = ex.generate(n, U, P, seed=20250204, zipf_s=1.1, lo=a, hi=b)
+    mask = MASK_COUNT | MASK_SUM | MASK_MEAN
+    cfg = BoundConfig(mask, L0, Linf, a, b, sampling_seed=13)
+    acc = ex.accumulate(pid, pk, val, U, P, cfg)
+    del pid, pk, val
+    eps = [0.0, 0.0, 0.5, 0.0, 0.0, 0.5]
+    delta = [0.0] * 5 + [1e-6]
+    off = ReleaseConfig(mask, native.NOISE_LAPLACE, native.SELECTION_TRUNCATED_GEOMETRIC, eps, delta, 1,
+                        add_noise=False, noise_seed=3)
+    keep0, out0, fields = ex.release(acc, off, cfg)
+    torch.cuda.synchronize()
+    assert fields == ["mean", "count", "sum"]
+    cnt = acc.count.to(torch.float64)
+    mean = acc.x / torch.clamp(cnt, min=1.0) + (a + (b - a) / 2)
+    assert torch.equal(out0[1], cnt)
+    assert bool(((out0[0] - mean).abs() <= 1e-12 * mean.abs().clamp(min=1.0)).all())
+    assert torch.equal(keep0.bool(), acc.row_count > 0)  # noise-free: keep iff p(n) > 0
+
+    on = ReleaseConfig(mask, native.NOISE_LAPLACE, native.SELECTION_TRUNCATED_GEOMETRIC, eps, delta, 1,
+                       add_noise=True, noise_seed=4)
+    keep, out, _ = ex.release(acc, on, cfg)
+    torch.cuda.synchronize()
+    table = torch.tensor(o.truncated_geometric_table(0.5, 1e-6, L0), dtype=torch.float64, device=acc.count.device)
+    rc = acc.row_count
+    p = torch.where(rc < len(table), table[rc.clamp(max=len(table) - 1)], torch.ones_like(table[:1]))
+    expect, var = float(p.sum()), float((p * (1 - p)).sum())
+    kept = int(keep.sum())
+    assert abs(kept - expect) <= 5 * math.sqrt(var) + 1, (kept, expect, var)
+    # Laplace(b = L0 * Linf / eps_count) on the released counts, b = 4 * 2 / 0.25
+    resid = (out[1] - cnt).cpu().numpy()
+    bscale = L0 * Linf / 0.25
+    assert abs(np.mean(np.abs(resid)) - bscale) <= 5 * bscale / math.sqrt(P)
+
+
+def test_c4_shard_binding_invariants(ex):
+    """c4 shard (BASELINE configs[3] per GPU): 5e8 rows, 1.25e7 privacy ids,
+    5e7 Zipf(1.1) partitions, L0=32, Linf=4 -- the LDS partition cache under
+    real contention and k_unpack_counts over 5e7 partitions."""
+    import torch
+    from pipelinedp_amd.executor import BoundConfig
+    n, U, P, L0, Linf, a, b = 500_000_000, 12_500_000, 50_000_000, 32, 4, 0.0, 10.0
+    pid, pk, val = ex.generate(n, U, P, seed=0x5EED0004, zipf_s=1.1, lo=a, hi=b)
+    cfg = BoundConfig(MASK_COUNT | MASK_SUM | MASK_MEAN | MASK_PID, L0, Linf, a, b, sampling_seed=21)
+    acc = ex.accumulate(pid, pk, val, U, P, cfg)
+    torch.cuda.synchronize()
+    rc, cnt, nsum = acc.row_count, acc.count, acc.x
+    rows_pk = torch.bincount(pk, minlength=P)
+    keys = _pairs(torch, pid, pk, P)
+    del pid, val
+    npk = torch.bincount(keys // P, minlength=U)
+    assert int(npk.max()) > L0  # binding
+    assert int(rc.sum()) == int(npk.clamp(max=L0).sum())
+    assert bool((rc <= torch.bincount(keys % P, minlength=P)).all())
+    del keys, npk
+    assert bool((cnt >= rc).all())
+    assert bool((cnt <= torch.minimum(Linf * rc, rows_pk)).all())
+    assert bool((nsum.abs() <= cnt.to(torch.float64) * (b - a) / 2 + 1e-6).all())
+
+
+def test_c4_partitions_non_binding_exact(ex):
+    """5e7 Zipf(1.1) partitions with non-binding bounds (L0=32 -> LDS cache on):
+    count == bincount(pk), privacy-id count == distinct pids per pk (exact)."""
+    import torch
+    from pipelinedp_amd.executor import BoundConfig
+    n, U, P, L0, Linf = 200_000_000, 100_000_000, 50_000_000, 32, 4
+    pid, pk, val = ex.generate(n, U, P, seed=0x5EED0005, zipf_s=1.1, lo=0.0, hi=10.0)
+    keys = _pairs(torch, pid, pk, P)
+    assert int(torch.bincount(keys // P, minlength=U).max()) <= L0
+    _, mult = torch.unique_consecutive(torch.sort(pid * P + pk).values, return_counts=True)
+    assert int(mult.max()) <= Linf
+    del mult
+    cfg = BoundConfig(MASK_COUNT | MASK_SUM | MASK_PID, L0, Linf, 0.0, 10.0, sampling_seed=9)
+    acc = ex.accumulate(pid, pk, val, U, P, cfg)
+    torch.cuda.synchronize()
+    assert torch.equal(acc.count, torch.bincount(pk, minlength=P))
+    assert torch.equal(acc.row_count, torch.bincount(keys % P, minlength=P))
+    ref = torch.zeros(P, dtype=torch.float64, device=pid.device).index_add_(0, pk, val)
+    absref = torch.zeros_like(ref).index_add_(0, pk, val.abs())
+    assert bool(((acc.x - ref).abs() <= 1e-9 * (absref + 1.0)).all())

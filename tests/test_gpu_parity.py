@@ -320,3 +320,49 @@ def test_truncated_geometric_selection_rate(ex):
         p = table[nv] if nv < len(table) else 1.0
         m = sel.sum()
         assert abs(k[sel].mean() - p) <= 4 * math.sqrt(p * (1 - p) / m) + 1e-12, (nv, k[sel].mean(), p)
+
+
+# ---------------------------------------------------------------------------
+# Multi-GPU ingestion: pdp_shard_rows (device side of the privacy-id shuffle)
+# ---------------------------------------------------------------------------
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 8, 64])
+def test_shard_rows_is_stable_grouping_by_shard(ex, world):
+    import torch
+    from pipelinedp_amd.distributed import shard_of
+    n, U, P = 100003, 5000, 700
+    pid, pk, val = o.synth_rows(n, U, P, seed=40 + world, zipf_s=1.1)
+    spid, spk, sval, counts = ex.shard_rows(_dev(pid, torch), _dev(pk, torch), _dev(val, torch), world)
+    torch.cuda.synchronize()
+    dest = shard_of(pid, world)
+    order = np.argsort(dest, kind="stable")
+    assert counts == np.bincount(dest, minlength=world).tolist()
+    np.testing.assert_array_equal(spid.cpu().numpy(), pid[order])
+    np.testing.assert_array_equal(spk.cpu().numpy(), pk[order])
+    np.testing.assert_array_equal(sval.cpu().numpy(), val[order])
+    _, _, none, c2 = ex.shard_rows(_dev(pid, torch), _dev(pk, torch), None, world)
+    assert none is None and c2 == counts
+
+
+# ---------------------------------------------------------------------------
+# select_partitions: the reference's probabilistic end-to-end test
+# (tests/dp_engine_test.py:444-492) with the MI355X noise
+# ---------------------------------------------------------------------------
+
+
+@pytest.mark.parametrize("seed", range(5))
+def test_select_partitions_reference_scenario(seed):
+    import pipelinedp_amd as pdp
+    col = [(u, "pk-many-contribs") for u in range(25)]
+    col += [(100 + u // 10, "pk-many-contribs-few-users") for u in range(30)]
+    col += [(200 + u, "pk-few-contribs") for u in range(3)]
+    for i in range(30):
+        col += [(500 + u, f"few-contribs-after-bound{i}") for u in range(25)]
+    acct = pdp.NaiveBudgetAccountant(total_epsilon=1, total_delta=1e-5)
+    engine = pdp.DPEngine(acct, pdp.HipBackend(sampling_seed=1000 + seed, noise_seed=2000 + seed))
+    res = engine.select_partitions(col, pdp.SelectPartitionsParams(max_partitions_contributed=1),
+                                   pdp.DataExtractors(privacy_id_extractor=lambda x: x[0],
+                                                      partition_extractor=lambda x: x[1]))
+    acct.compute_budgets()
+    assert list(res) == ["pk-many-contribs"]

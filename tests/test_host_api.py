@@ -162,3 +162,51 @@ def test_host_encoding():
     e = encode_rows(rows, ex, public_partitions=["c", "zz", "a", "c"])
     assert e.partition_keys == ["c", "zz", "a"] and e.pk.tolist() == [2, -1, 0, 2]
     np.testing.assert_array_equal(e.value, [1, 2, 3, 4])
+
+
+def test_hip_backend_host_ops_follow_local_backend():
+    # LocalBackend.sample_fixed_per_key / combine_accumulators_per_key
+    # (pipeline_backend.py:504-538), element-wise on the host
+    b = pdp.HipBackend(sampling_seed=3)
+    col = [("a", i) for i in range(10)] + [("b", 1), ("b", 2)]
+    out = dict(b.sample_fixed_per_key(col, 3))
+    assert set(out) == {"a", "b"} and len(out["a"]) == 3 and len(set(out["a"])) == 3
+    assert set(out["a"]) <= set(range(10)) and sorted(out["b"]) == [1, 2]
+
+    class SumCombiner:
+
+        def merge_accumulators(self, a, b):
+            return a + b
+
+    merged = dict(b.combine_accumulators_per_key([("x", 1), ("y", 5), ("x", 2), ("x", 3)], SumCombiner()))
+    assert merged == {"x": 6, "y": 5}
+    assert sorted(b.sum_per_key([("x", 1), ("x", 2), ("y", 3)])) == [("x", 3), ("y", 3)]
+
+
+def _engine_with_cpu_executor():
+    from cpu_executor import CpuExecutor
+    backend = pdp.HipBackend(sampling_seed=1, noise_seed=2)
+    backend._executor = CpuExecutor()
+    acct = pdp.NaiveBudgetAccountant(total_epsilon=1, total_delta=1e-6)
+    return pdp.DPEngine(acct, backend), acct
+
+
+def test_empty_public_partitions_give_empty_result():
+    # reference: public_partitions=[] drops every row and adds no partition
+    engine, acct = _engine_with_cpu_executor()
+    params = pdp.AggregateParams(metrics=[M.COUNT], max_partitions_contributed=1, max_contributions_per_partition=1)
+    ex = pdp.DataExtractors(privacy_id_extractor=lambda r: r[0], partition_extractor=lambda r: r[1],
+                            value_extractor=lambda r: 0)
+    res = engine.aggregate([(1, "a"), (2, "b")], params, ex, public_partitions=[])
+    acct.compute_budgets()
+    assert list(res) == []
+
+
+def test_columnar_partition_out_of_range_raises():
+    engine, acct = _engine_with_cpu_executor()
+    params = pdp.AggregateParams(metrics=[M.COUNT], max_partitions_contributed=1, max_contributions_per_partition=1)
+    col = pdp.ColumnarData(partition=np.array([0, 1, 5]), privacy_id=np.array([0, 1, 2]), num_partitions=3)
+    res = engine.aggregate(col, params, None, public_partitions=[0, 1])
+    acct.compute_budgets()
+    with pytest.raises(ValueError, match="num_partitions"):
+        list(res)

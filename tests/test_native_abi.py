@@ -72,3 +72,28 @@ def test_library_fails_loudly_when_missing(monkeypatch, tmp_path):
     monkeypatch.setattr(native, "LIB_PATH", str(tmp_path / "missing.so"))
     with pytest.raises(native.NativeError):
         native.lib()
+
+
+@pytest.mark.parametrize("k", [1, 2, 4, 32])
+def test_one_delta_adjustment_for_all_selection_strategies(k):
+    # truncated geometric p(1) = adjusted delta (from p(0) = 0), and the
+    # Laplace threshold inverts the same adjusted delta: one per-partition
+    # (eps / k, 1 - (1 - delta)^(1/k)) rule for the three strategies.
+    eps, delta = 1.0, 1e-5
+    adj = o.adjusted_delta(delta, k)
+    assert adj == (delta if k == 1 else pytest.approx(1 - (1 - delta)**(1 / k), rel=1e-9))
+    assert abs(adj - delta / k) <= delta**2
+    t = native.truncated_geometric_table(eps, delta, k)
+    assert t[1] == pytest.approx(adj, rel=1e-12)
+    thr, b = native.selection_threshold(2, eps, delta, k)
+    assert b == k / eps
+    # P(1 + Lap(b) > thr) == adjusted delta (Laplace tail)
+    assert 0.5 * math.exp(-(thr - 1) / b) == pytest.approx(adj, rel=1e-9)
+
+
+def test_shard_symbols_reject_bad_args():
+    import ctypes
+    n = ctypes.c_size_t(0)
+    assert native.lib().pdp_shard_workspace_size(1000, 0, ctypes.byref(n)) != 0
+    assert native.lib().pdp_shard_workspace_size(1000, 65, ctypes.byref(n)) != 0
+    assert native.lib().pdp_shard_workspace_size(1000, 8, ctypes.byref(n)) == 0 and n.value > 0

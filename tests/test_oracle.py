@@ -167,3 +167,21 @@ def test_binding_bounds_match_reference_distribution():
     se = np.sqrt(ref_std**2 / int(d["runs"]) + res.std(0)**2 / runs) + 1e-9
     z = np.abs(res.mean(0) - ref_mean) / se
     assert z.max() < 5.0, z.max()
+
+
+@pytest.mark.parametrize("kind,scale", [("laplace", 3.7), ("laplace", 1024.0), ("gaussian", 2.5)])
+def test_snapped_noise_is_on_grid_and_distributed_right(kind, scale):
+    # granularity snapping (pdp_rng.h:add_snapped_noise): outputs are
+    # multiples of g = 2^(ceil(log2 scale) - 40); the distribution is the
+    # reference's (KS p >= 0.001, tests/dp_computations_test.py:69-83)
+    from scipy import stats
+    g = o.noise_grid(scale)
+    assert g == 2.0**(math.ceil(math.log2(scale)) - 40)
+    n = 200000
+    x = o.add_snapped_noise(kind, np.full(n, 10.0 + g / 3), seed=77, idx=np.arange(n), stream=3, scale=scale) - 10.0
+    assert np.all(np.rint(x / g) * g == x)
+    ref = stats.laplace(scale=scale) if kind == "laplace" else stats.norm(scale=scale)
+    assert stats.kstest(x, ref.cdf).pvalue >= 0.001
+    # tails beyond the 36.7-scale cap of a 53-bit inverse CDF are reachable
+    u = o._uniform64(np.uint64(0), np.uint64(1))
+    assert -math.log(float(u)) > 43
