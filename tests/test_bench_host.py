@@ -39,5 +39,7 @@ def test_sweep_grid_is_64_configs():
 def test_cpu_baseline_leg_runs(w):
     a = _parse("--workload", w, "--cpu-sample", "3000", "--partitions", "500")
     res = bench.cpu_baseline(a, int(a.partitions))
-    assert res["value"] > 0 and res["kind"] == "port" and res["cores"] == 1
+    assert res["value"] > 0 and res["kind"] == "port" and res["plan_item"] == 3
+    # every host core (up to the GPU box's 16-core share), reported with the CPU model
+    assert 1 <= res["cores"] <= 16 and res["host_cpus_visible"] >= res["cores"]
     assert res["sample"].startswith(w)

@@ -166,7 +166,7 @@ def test_c4_partitions_non_binding_exact(ex):
     count == bincount(pk), privacy-id count == distinct pids per pk (exact)."""
     import torch
     from pipelinedp_amd.executor import BoundConfig
-    n, U, P, L0, Linf = 200_000_000, 100_000_000, 50_000_000, 32, 4
+    n, U, P, L0, Linf = 200_000_000, 100_000_000, 50_000_000, 32, 16
     pid, pk, val = ex.generate(n, U, P, seed=0x5EED0005, zipf_s=1.1, lo=0.0, hi=10.0)
     keys = _pairs(torch, pid, pk, P)
     assert int(torch.bincount(keys // P, minlength=U).max()) <= L0
@@ -178,6 +178,10 @@ def test_c4_partitions_non_binding_exact(ex):
     torch.cuda.synchronize()
     assert torch.equal(acc.count, torch.bincount(pk, minlength=P))
     assert torch.equal(acc.row_count, torch.bincount(keys % P, minlength=P))
-    ref = torch.zeros(P, dtype=torch.float64, device=pid.device).index_add_(0, pk, val)
-    absref = torch.zeros_like(ref).index_add_(0, pk, val.abs())
-    assert bool(((acc.x - ref).abs() <= 1e-9 * (absref + 1.0)).all())
+    # fp64 reference sums on the host: torch's device index_add_ serialises on
+    # the Zipf head partition (same-address fp64 atomics)
+    import numpy as np
+    pkh, valh = pk.cpu().numpy(), val.cpu().numpy()
+    ref = np.bincount(pkh, weights=valh, minlength=P)
+    absref = np.bincount(pkh, weights=np.abs(valh), minlength=P)
+    assert np.all(np.abs(acc.x.cpu().numpy() - ref) <= 1e-9 * (absref + 1.0))
