@@ -195,5 +195,53 @@ def main():
     print(f"binding: {runs} runs, fields={fields}")
 
 
+def run_select_partitions(pid, pk, L0, threshold, seed=None):
+    """Reference DPEngine.select_partitions (dp_engine.py:204-281) with the
+    stub's deterministic strategy keep(n) = n >= threshold."""
+    if seed is not None:
+        np.random.seed(seed)
+    os.environ["PDP_STUB_SELECT_THRESHOLD"] = str(threshold)
+    try:
+        acct = pipeline_dp.NaiveBudgetAccountant(total_epsilon=1.0, total_delta=1e-6)
+        engine = pipeline_dp.DPEngine(acct, pipeline_dp.LocalBackend())
+        ex = pipeline_dp.DataExtractors(privacy_id_extractor=lambda r: r[0], partition_extractor=lambda r: r[1])
+        res = engine.select_partitions([(int(a), int(b)) for a, b in zip(pid, pk)],
+                                       pipeline_dp.SelectPartitionsParams(max_partitions_contributed=L0), ex)
+        acct.compute_budgets()
+        return sorted(int(k) for k in res)
+    finally:
+        del os.environ["PDP_STUB_SELECT_THRESHOLD"]
+
+
+def select_partitions_cases():
+    """select_partitions goldens: non-binding L0 (exact kept set) and binding
+    L0 (per-partition inclusion frequency over 400 numpy seeds)."""
+    rng = np.random.default_rng(20250205)
+    n, U, P = 8000, 600, 300
+    pid = rng.integers(0, U, n)
+    pk = np.minimum(rng.zipf(1.4, n) - 1, P - 1)
+    L0, _ = nonbinding(pid, pk)
+    T = 3
+    kept = run_select_partitions(pid, pk, L0, T)
+    np.savez_compressed(os.path.join(OUT, "select_partitions_nonbinding.npz"), pid=pid, pk=pk,
+                        out_keys=np.asarray(kept, np.int64),
+                        meta=np.asarray(json.dumps(dict(L0=L0, threshold=T, P=P))))
+    print(f"select_partitions_nonbinding: {n} rows, L0={L0}, {len(kept)} kept")
+    nb, Ub, Pb, L0b, Tb, runs = 900, 60, 15, 1, 5, 400
+    pidb = rng.integers(0, Ub, nb)
+    pkb = rng.integers(0, Pb, nb)
+    freq = np.zeros(Pb)
+    for s in range(runs):
+        for k in run_select_partitions(pidb, pkb, L0b, Tb, seed=s):
+            freq[k] += 1
+    np.savez_compressed(os.path.join(OUT, "select_partitions_binding.npz"), pid=pidb, pk=pkb, freq=freq / runs,
+                        runs=runs, meta=np.asarray(json.dumps(dict(L0=L0b, threshold=Tb, P=Pb))))
+    print(f"select_partitions_binding: {runs} runs, inclusion frequencies {np.round(freq / runs, 3)}")
+
+
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) > 1 and sys.argv[1] == "select":
+        select_partitions_cases()
+    else:
+        main()
+        select_partitions_cases()

@@ -366,3 +366,36 @@ def test_select_partitions_reference_scenario(seed):
                                                       partition_extractor=lambda x: x[1]))
     acct.compute_budgets()
     assert list(res) == ["pk-many-contribs"]
+
+
+def _gpu_select_counts(ex, pid, pk, P, L0, seed):
+    import torch
+    from pipelinedp_amd.executor import BoundConfig
+    U = int(pid.max()) + 1
+    acc = ex.accumulate(_dev(pid, torch), _dev(pk, torch), None, U, P, BoundConfig(0, L0, 1, sampling_seed=seed))
+    return acc.row_count.cpu().numpy()
+
+
+def test_select_partitions_counts_match_reference_golden(ex):
+    d = load("select_partitions_nonbinding")
+    meta = d["meta"]
+    rc = _gpu_select_counts(ex, d["pid"], d["pk"], meta["P"], meta["L0"], seed=3)
+    assert np.flatnonzero(rc >= meta["threshold"]).tolist() == d["out_keys"].tolist()
+
+
+def test_select_partitions_binding_matches_reference_distribution_on_gpu(ex):
+    d = load("select_partitions_binding")
+    meta = d["meta"]
+    runs = int(d["runs"])
+    freq = np.zeros(meta["P"])
+    for s in range(runs):
+        rc = _gpu_select_counts(ex, d["pid"], d["pk"], meta["P"], meta["L0"], seed=5000 + s)
+        if s < 5:  # the GPU sampler is the oracle's, bit for bit
+            np.testing.assert_array_equal(rc, o.bound_and_accumulate(d["pid"], d["pk"], None, meta["P"],
+                                                                     o.BoundParams(meta["L0"], 1), "hash",
+                                                                     seed=5000 + s).row_count)
+        freq += rc >= meta["threshold"]
+    freq /= runs
+    p = (freq + d["freq"]) / 2
+    sd = np.sqrt(2 * p * (1 - p) / runs) + 1e-9
+    assert np.all(np.abs(freq - d["freq"]) <= 4.5 * sd), (freq, d["freq"])

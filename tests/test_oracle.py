@@ -1,14 +1,16 @@
 """Pins the CPU oracle (oracle/pdp_oracle.py) against the reference:
 golden vectors produced by the reference LocalBackend (oracle/gen_golden.py)
 and the known-answer numbers of the reference's own tests."""
+import json
 import math
+import os
 
 import numpy as np
 import pytest
 from scipy.stats import binom
 
 import pdp_oracle as o
-from golden_util import aggregate_cases, encode_case, known_answers, load, sum_tolerance
+from golden_util import GOLDEN, aggregate_cases, encode_case, known_answers, load, sum_tolerance
 
 
 def oracle_run(d, sampler="hash", seed=0, noise=False):
@@ -185,3 +187,29 @@ def test_snapped_noise_is_on_grid_and_distributed_right(kind, scale):
     # tails beyond the 36.7-scale cap of a 53-bit inverse CDF are reachable
     u = o._uniform64(np.uint64(0), np.uint64(1))
     assert -math.log(float(u)) > 43
+
+
+def _select_counts(pid, pk, P, L0, seed):
+    # select_partitions (dp_engine.py:229-281): per pid <= L0 distinct pks,
+    # then privacy ids per pk -- the row_count of a COUNT-less bound
+    return o.bound_and_accumulate(pid, pk, None, P, o.BoundParams(L0, 1), "hash", seed=seed).row_count
+
+
+def test_select_partitions_matches_reference_golden():
+    d = np.load(os.path.join(GOLDEN, "select_partitions_nonbinding.npz"))
+    meta = json.loads(str(d["meta"]))
+    rc = _select_counts(d["pid"], d["pk"], meta["P"], meta["L0"], seed=3)
+    assert np.flatnonzero(rc >= meta["threshold"]).tolist() == d["out_keys"].tolist()
+
+
+def test_select_partitions_binding_matches_reference_distribution():
+    d = np.load(os.path.join(GOLDEN, "select_partitions_binding.npz"))
+    meta = json.loads(str(d["meta"]))
+    runs = int(d["runs"])
+    freq = np.zeros(meta["P"])
+    for s in range(runs):
+        freq += _select_counts(d["pid"], d["pk"], meta["P"], meta["L0"], seed=1000 + s) >= meta["threshold"]
+    freq /= runs
+    p = (freq + d["freq"]) / 2
+    sd = np.sqrt(2 * p * (1 - p) / runs) + 1e-9
+    assert np.all(np.abs(freq - d["freq"]) <= 4.5 * sd), (freq, d["freq"])
