@@ -199,6 +199,70 @@ int pdp_truncated_geometric_table(double eps, double delta, int64_t max_partitio
 int pdp_selection_threshold(int32_t selection, double eps, double delta, int64_t max_partitions,
                             double* threshold, double* scale);
 
+/* Utility analysis (BASELINE.json configs[4]): the per-partition metrics of
+ * the reference's UtilityAnalysisEngine.analyze
+ * (analysis/utility_analysis_engine.py:53-173) for many bounding
+ * configurations in one launch sequence:
+ *   rows -> per (privacy id, partition) (count, sum, n_partitions)
+ *     (SamplingL0LinfContributionBounder, analysis/contribution_bounders.py:38-75;
+ *      analysis/pre_aggregation.py:preaggregate)
+ *   -> per configuration c and partition p, for each of SUM, COUNT,
+ *      PRIVACY_ID_COUNT in mask order SUM, COUNT, PRIVACY_ID_COUNT:
+ *      (sum, per_partition_error_min, per_partition_error_max,
+ *       expected_cross_partition_error, var_cross_partition_error)
+ *      (SumCombiner / CountCombiner / PrivacyIdCountCombiner,
+ *       analysis/combiners.py:228-310; std = sqrt(var))
+ *   -> with private selection: the keep probability
+ *      (PartitionSelectionCombiner + Poisson binomial, analysis/combiners.py:
+ *       99-225, analysis/poisson_binomial.py:39-83).
+ * metrics[C][nb][5][P] and prob_keep[C][P] are device arrays; nb = number of
+ * metrics in the mask.  Every configuration uses private selection
+ * (selection != NONE: partitions present in the data) or none does (public
+ * partitions: pk in [0, P) are the public partitions; rows with pk < 0 are
+ * dropped, every partition gets the empty accumulator's pseudo-contribution
+ * (0, 0, 0) as in analysis/combiners.py:337-342).  Partition sampling:
+ * partitions [num_sampled_partitions, P) count toward n_partitions but are
+ * not analysed (ValueSampler, pipeline_dp/sampling_utils.py:38-51, decided on
+ * the host).  std_noise is host arithmetic (dp_computations.py:462-481). */
+typedef struct pdp_analysis_config {
+  int64_t max_partitions_contributed;       /* L0: keep probability q = min(1, L0 / n_partitions) */
+  int64_t max_contributions_per_partition;  /* COUNT clip [0, L_inf] */
+  double min_sum_per_partition, max_sum_per_partition;  /* SUM clip */
+  int32_t selection;                        /* PDP_SELECTION_*; NONE = public partitions */
+  int32_t reserved;
+  double selection_eps, selection_delta;    /* the GENERIC mechanism's budget */
+} pdp_analysis_config;
+
+typedef struct pdp_analysis_outputs {
+  double* metrics;         /* [num_configs][nb][5][num_partitions] */
+  double* prob_keep;       /* [num_configs][num_partitions]; private selection only */
+  int64_t* privacy_ids;    /* [num_partitions] privacy ids with data in the partition (optional) */
+} pdp_analysis_outputs;
+
+int pdp_analysis_workspace_size(int64_t num_rows, int64_t num_privacy_ids, int64_t num_partitions,
+                                const pdp_analysis_config* cfgs, int32_t num_configs, size_t* bytes);
+int pdp_utility_analysis(pdp_ctx* ctx, const pdp_columns* cols, int64_t num_sampled_partitions, int32_t metrics,
+                         const pdp_analysis_config* cfgs, int32_t num_configs, const pdp_analysis_outputs* out,
+                         void* workspace, size_t workspace_bytes, void* stream);
+/* Pre-aggregated input (options.pre_aggregated_data, NoOpContributionBounder,
+ * analysis/contribution_bounders.py:78-88): one row per (privacy id,
+ * partition) with (count, sum, n_partitions).  Workspace:
+ * pdp_analysis_workspace_size(num_pairs, num_pairs, ...). */
+int pdp_utility_analysis_preaggregated(pdp_ctx* ctx, const int64_t* pk, const int64_t* count, const double* sum,
+                                       const int64_t* n_partitions, int64_t num_pairs, int64_t num_partitions,
+                                       int32_t metrics, const pdp_analysis_config* cfgs, int32_t num_configs,
+                                       const pdp_analysis_outputs* out, void* workspace, size_t workspace_bytes,
+                                       void* stream);
+
+/* analysis/pre_aggregation.py:preaggregate: one (pk, count, sum, n_partitions)
+ * per (privacy id, partition) of a sampled partition (pk < num_sampled), in
+ * (pk, privacy id) order; out_* hold num_rows entries, *num_pairs (host) is
+ * set.  Workspace: pdp_analysis_workspace_size with one configuration of
+ * selection NONE. */
+int pdp_preaggregate(pdp_ctx* ctx, const pdp_columns* cols, int64_t num_sampled_partitions, int64_t* out_pk,
+                     int64_t* out_count, double* out_sum, int64_t* out_n_partitions, int64_t* num_pairs,
+                     void* workspace, size_t workspace_bytes, void* stream);
+
 /* Multi-GPU ingestion of rows that are not sharded by privacy id: the device
  * side of the reference's group-by-pid shuffles (BeamBackend / SparkRDDBackend
  * / LocalBackend.group_by_key, pipeline_dp/pipeline_backend.py:261, 401,
@@ -243,7 +307,9 @@ enum {
   PDP_STAGE_RELEASE = 5,         /* K5/K6 */
   PDP_STAGE_ENFORCED = 6,        /* bounds already enforced accumulate */
   PDP_STAGE_TILE_COUNTS = 7,     /* K1u per-tile digit counts (passes >= 1) + tile-offset scans */
-  PDP_NUM_STAGES = 8,
+  PDP_STAGE_ANALYSIS_PAIRS = 8,  /* utility analysis: (pk, pid) sort + per-pair pre-aggregation */
+  PDP_STAGE_ANALYSIS_METRICS = 9, /* utility analysis: per-configuration partition metrics + selection */
+  PDP_NUM_STAGES = 10,
 };
 int pdp_profile_enable(pdp_ctx* ctx, int enable);
 /* Waits for recorded events; adds into ms_out/launches_out[PDP_NUM_STAGES]

@@ -239,9 +239,145 @@ def select_partitions_cases():
     print(f"select_partitions_binding: {runs} runs, inclusion frequencies {np.round(freq / runs, 3)}")
 
 
+def run_analysis(rows, extractors, cfg, multi=None, public=None, pre_aggregated=False, sampling=1.0):
+    """Reference UtilityAnalysisEngine.analyze (analysis/utility_analysis_engine.py:53-86)
+    -> keys and per-partition arrays: prob [C, P] (private only) and, per
+    metric of (SUM, COUNT, PRIVACY_ID_COUNT) present, [C, 6, P] of
+    (sum, err_min, err_max, expected_cross, std_cross, std_noise)."""
+    import analysis
+    from analysis import utility_analysis_engine
+    acct = pipeline_dp.NaiveBudgetAccountant(total_epsilon=cfg["eps"], total_delta=cfg["delta"])
+    engine = utility_analysis_engine.UtilityAnalysisEngine(acct, pipeline_dp.LocalBackend())
+    kw = dict(metrics=[METRIC[m] for m in cfg["metrics"]],
+              noise_kind=pipeline_dp.NoiseKind(cfg.get("noise_kind", "laplace")),
+              max_partitions_contributed=cfg["L0"], max_contributions_per_partition=cfg["Linf"])
+    for k in ("min_sum_per_partition", "max_sum_per_partition"):
+        if cfg.get(k) is not None:
+            kw[k] = cfg[k]
+    if cfg.get("selection"):
+        kw["partition_selection_strategy"] = pipeline_dp.PartitionSelectionStrategy[cfg["selection"].upper()]
+    params = pipeline_dp.AggregateParams(**kw)
+    mp = None
+    if multi:
+        mk = dict(multi)
+        if "partition_selection_strategy" in mk:
+            mk["partition_selection_strategy"] = [pipeline_dp.PartitionSelectionStrategy[v.upper()]
+                                                  for v in mk["partition_selection_strategy"]]
+        if "noise_kind" in mk:
+            mk["noise_kind"] = [pipeline_dp.NoiseKind(v) for v in mk["noise_kind"]]
+        mp = analysis.MultiParameterConfiguration(**mk)
+    options = analysis.UtilityAnalysisOptions(epsilon=cfg["eps"], delta=cfg["delta"], aggregate_params=params,
+                                              multi_param_configuration=mp, partitions_sampling_prob=sampling,
+                                              pre_aggregated_data=pre_aggregated)
+    out = engine.analyze(rows, options, extractors, public_partitions=public)
+    acct.compute_budgets()
+    out = sorted(list(out), key=lambda kv: kv[0])
+    C = options.n_configurations
+    present = [m for m in ("sum", "count", "privacy_id_count") if m in cfg["metrics"]]
+    per = (0 if public is not None else 1) + len(present)
+    P = len(out)
+    keys = np.array([k for k, _ in out], dtype=np.int64)
+    prob = np.zeros((C, P))
+    arr = {m: np.zeros((C, 6, P)) for m in present}
+    for p, (_, vals) in enumerate(out):
+        vals = list(vals)
+        assert len(vals) == C * per, (len(vals), C, per)
+        for c in range(C):
+            chunk = vals[c * per:(c + 1) * per]
+            if public is None:
+                prob[c, p] = float(chunk[0])
+                chunk = chunk[1:]
+            for m, sm in zip(present, chunk):
+                arr[m][c, :, p] = (sm.sum, sm.per_partition_error_min, sm.per_partition_error_max,
+                                   sm.expected_cross_partition_error, sm.std_cross_partition_error, sm.std_noise)
+    return keys, prob, arr
+
+
+def save_analysis(name, pid, pk, value, cfg, multi=None, public=None, sampling=1.0, pre=None):
+    if pre is not None:  # pre-aggregated rows (pk, (count, sum, n_partitions))
+        rows = [(int(a), (int(b), float(c), int(d))) for a, b, c, d in zip(*pre)]
+        ex = analysis_pre_extractors()
+        keys, prob, arr = run_analysis(rows, ex, cfg, multi, public, pre_aggregated=True, sampling=sampling)
+    else:
+        rows = [(int(a), int(b), float(v)) for a, b, v in zip(pid, pk, value)]
+        ex = pipeline_dp.DataExtractors(privacy_id_extractor=lambda r: r[0], partition_extractor=lambda r: r[1],
+                                        value_extractor=lambda r: r[2])
+        keys, prob, arr = run_analysis(rows, ex, cfg, multi, public, sampling=sampling)
+    z = np.zeros(0)
+    np.savez_compressed(
+        os.path.join(OUT, "analysis_" + name + ".npz"),
+        pid=np.asarray(pid if pid is not None else z, np.int64), pk=np.asarray(pk if pk is not None else z, np.int64),
+        value=np.asarray(value if value is not None else z, np.float64),
+        pre=np.asarray(pre if pre is not None else np.zeros((4, 0)), np.float64),
+        public=np.asarray(public if public is not None else [], np.int64), has_public=np.asarray(public is not None),
+        out_keys=keys, prob=prob, **{"m_" + m: a for m, a in arr.items()},
+        meta=np.asarray(json.dumps(dict(cfg=cfg, multi=multi, sampling=sampling, metrics=list(arr)))))
+    print(f"analysis_{name}: {len(keys)} partitions, metrics={list(arr)}")
+
+
+def analysis_pre_extractors():
+    import analysis
+    return analysis.PreAggregateExtractors(partition_extractor=lambda r: r[0], preaggregate_extractor=lambda r: r[1])
+
+
+def analysis_cases():
+    """Utility-analysis goldens (configs[4]); see pdp_analysis_oracle.py."""
+    # A. analysis/tests/utility_analysis_engine_test.py:157-220 (known answers)
+    rows = [(i, j) for i in range(10) for j in range(10)] * 3
+    save_analysis("reference_per_partition_errors", [r[0] for r in rows], [r[1] for r in rows],
+                  [0.0] * len(rows),
+                  dict(metrics=["count"], L0=1, Linf=2, eps=2.0, delta=1e-10, noise_kind="gaussian"))
+    # B. :222-302 (multi parameters, public partitions)
+    save_analysis("reference_multi_parameters", [0, 0, 0], [0, 1, 1], [0.0] * 3,
+                  dict(metrics=["count"], L0=1, Linf=1, eps=1.0, delta=1e-10, noise_kind="gaussian"),
+                  multi=dict(max_partitions_contributed=[1, 2], max_contributions_per_partition=[1, 2]),
+                  public=[0, 1])
+    rng = np.random.default_rng(20250206)
+    # C. private selection, 6 configs incl. the thresholding strategies, partitions with > 100 privacy ids
+    n, U, P = 12000, 800, 60
+    pid = rng.integers(0, U, n)
+    pk = np.minimum(rng.zipf(1.5, n) - 1, P - 1)
+    val = rng.normal(2.0, 3.0, n)
+    save_analysis("private_multi", pid, pk, val,
+                  dict(metrics=["count", "sum", "privacy_id_count"], L0=2, Linf=2, eps=3.0, delta=1e-5,
+                       noise_kind="gaussian", min_sum_per_partition=-3.0, max_sum_per_partition=5.0),
+                  multi=dict(max_partitions_contributed=[1, 2, 3, 5, 2, 4],
+                             max_contributions_per_partition=[1, 2, 3, 1, 2, 4],
+                             min_sum_per_partition=[-3.0, 0.0, -1.0, 1.0, -2.0, 0.5],
+                             max_sum_per_partition=[5.0, 2.0, 4.0, 3.0, 8.0, 0.75],
+                             partition_selection_strategy=["truncated_geometric", "truncated_geometric",
+                                                           "laplace_thresholding", "gaussian_thresholding",
+                                                           "truncated_geometric", "laplace_thresholding"]))
+    # D. public partitions (absent ones too) with SUM bounds excluding 0 (the empty accumulator matters)
+    save_analysis("public_sum", pid, pk, val,
+                  dict(metrics=["sum", "count"], L0=3, Linf=2, eps=1.0, delta=1e-6, noise_kind="laplace",
+                       min_sum_per_partition=0.5, max_sum_per_partition=6.0),
+                  public=list(range(0, P, 2)) + [P + 3, P + 9])
+    # E. pre-aggregated input (NoOpContributionBounder)
+    gp, gc, gs, gn = [], [], [], []
+    for i in range(300):
+        npart = int(rng.integers(1, 6))
+        for k in rng.choice(40, npart, replace=False):
+            gp.append(int(k))
+            gc.append(int(rng.integers(1, 5)))
+            gs.append(float(rng.normal(1.0, 2.0)))
+            gn.append(npart)
+    save_analysis("pre_aggregated", None, None, None,
+                  dict(metrics=["count", "privacy_id_count", "sum"], L0=2, Linf=2, eps=1.0, delta=1e-6,
+                       noise_kind="laplace", min_sum_per_partition=-1.0, max_sum_per_partition=2.0),
+                  pre=np.array([gp, gc, gs, gn], dtype=np.float64))
+    # F. partition sampling (ValueSampler, sampling_utils.py:38-51)
+    save_analysis("partition_sampling", pid, pk, val,
+                  dict(metrics=["count"], L0=2, Linf=3, eps=1.0, delta=1e-6, noise_kind="laplace"),
+                  sampling=0.5)
+
+
 if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "select":
         select_partitions_cases()
+    elif len(sys.argv) > 1 and sys.argv[1] == "analysis":
+        analysis_cases()
     else:
         main()
         select_partitions_cases()
+        analysis_cases()

@@ -62,6 +62,7 @@ enum Counter {
   kCtrBigNext = 7,
   kCtrSweepCycles = 8,  // 8..11: onesweep load / rank / look-back / scatter cycles (profiling)
   kCtrSweepTiles = 12,
+  kCtrAnaPairs = 13,  // utility analysis: pairs of sampled partitions
   kCtrTile0 = 16,  // 16..63 tile claim counters, one per onesweep launch
 };
 
@@ -735,6 +736,7 @@ __device__ __forceinline__ void emit_group(const SegParams& sp, const AccPtrs& a
 }
 
 #include "pdp_segments.inc"
+#include "pdp_analysis.inc"
 
 // ---------------------------------------------------------------------------
 // KF: generic sorted-stream path (fallback for buckets that overflow LDS)
@@ -1960,6 +1962,233 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
   return 0;
 }
 
+// ---------------------------------------------------------------------------
+// Utility analysis host side (pdp_analysis.inc)
+// ---------------------------------------------------------------------------
+
+// Keep probability table of a selection strategy for k = L0 partitions:
+// keep[i] for i < len, 1 beyond (PyDP probability_of_keep restated, the
+// functions of the utility analysis' PartitionSelectionCalculator,
+// analysis/combiners.py:124-141).
+int keep_table(int selection, double eps, double delta, int64_t k, std::vector<double>& t) {
+  t.clear();
+  if (selection == PDP_SELECTION_NONE) return 0;
+  if (selection == PDP_SELECTION_TRUNCATED_GEOMETRIC) {
+    int64_t len = 0;
+    if (int rc = pdp_truncated_geometric_table(eps, delta, k, nullptr, 0, &len)) return rc;
+    t.assign((size_t)len, 0.0);
+    return pdp_truncated_geometric_table(eps, delta, k, t.data(), len, &len);
+  }
+  double thr = 0, scale = 0;
+  if (int rc = pdp_selection_threshold(selection, eps, delta, k, &thr, &scale)) return rc;
+  t.push_back(0.0);  // n = 0 is never kept
+  for (int64_t i = 1;; ++i) {
+    const double x = thr - (double)i;
+    double p;
+    if (selection == PDP_SELECTION_LAPLACE_THRESHOLDING)
+      p = x >= 0 ? 0.5 * std::exp(-std::fabs(x) / scale) : 1.0 - 0.5 * std::exp(-std::fabs(x) / scale);
+    else
+      p = 0.5 * std::erfc(x / (scale * std::sqrt(2.0)));
+    if (p >= 1.0) break;
+    t.push_back(p);
+    if (t.size() > (1u << 24)) return fail(PDP_ERR_INVALID_ARG, "selection keep table too long (eps too small)");
+  }
+  return 0;
+}
+
+struct AnaLayout {
+  size_t recs_a, recs_b, flags, ppk, pref, pcnt, psum, npart, pbeg, mom, cfg, keep, hist, off, counters, status, total;
+  int64_t tiles;
+  std::vector<AnaCfg> cfgs;  // keep pointers are offsets until bound to the workspace
+  std::vector<double> keep_all;
+};
+
+int ana_layout(int64_t n, int64_t U, int64_t P, const pdp_analysis_config* cfgs, int nconf, AnaLayout& L) {
+  size_t o = 0;
+  const size_t n1 = (size_t)std::max<int64_t>(n, 1);
+  auto take = [&](size_t bytes) {
+    const size_t at = o;
+    o += align_up(std::max<size_t>(bytes, 8), 256);
+    return at;
+  };
+  L.recs_a = take(n1 * sizeof(Rec));
+  L.recs_b = take(n1 * sizeof(Rec));
+  L.flags = take(n1 * 8);
+  L.ppk = take(n1 * 4);
+  L.pref = take(n1 * 4);
+  L.pcnt = take(n1 * 4);
+  L.psum = take(n1 * 8);
+  L.npart = take((size_t)std::max<int64_t>(U, 1) * 4);
+  L.pbeg = take((size_t)(P + 1) * 8);
+  const bool priv = nconf > 0 && cfgs[0].selection != PDP_SELECTION_NONE;
+  L.mom = take(priv ? (size_t)nconf * 4 * P * 8 : 8);
+  L.cfg = take((size_t)nconf * sizeof(AnaCfg));
+  L.cfgs.assign((size_t)nconf, AnaCfg{});
+  L.keep_all.clear();
+  std::vector<double> t;
+  for (int c = 0; c < nconf; ++c) {
+    const pdp_analysis_config& a = cfgs[c];
+    if ((a.selection != PDP_SELECTION_NONE) != priv)
+      return fail(PDP_ERR_INVALID_ARG, "all configurations must use private selection, or none (public partitions)");
+    if (a.max_partitions_contributed < 1 || a.max_contributions_per_partition < 1)
+      return fail(PDP_ERR_INVALID_ARG, "contribution bounds must be positive");
+    if (int rc = keep_table(a.selection, a.selection_eps, a.selection_delta, a.max_partitions_contributed, t)) return rc;
+    AnaCfg& g = L.cfgs[c];
+    g.l0 = (double)a.max_partitions_contributed;
+    g.linf = (double)a.max_contributions_per_partition;
+    g.smin = a.min_sum_per_partition;
+    g.smax = a.max_sum_per_partition;
+    g.keep = (const double*)(uintptr_t)L.keep_all.size();  // offset, bound later
+    g.keep_len = (int64_t)t.size();
+    L.keep_all.insert(L.keep_all.end(), t.begin(), t.end());
+  }
+  L.keep = take(L.keep_all.size() * 8);
+  L.hist = take(kMaxPasses * kHist * 8);
+  L.off = take(kMaxPasses * kHist * 8);
+  L.counters = take(kNumCounters * 8);
+  L.tiles = (int64_t)(n1 + kTile - 1) / kTile;
+  L.status = take((size_t)L.tiles * kStatusStride * 8);
+  L.total = o;
+  return 0;
+}
+
+// Raw rows (pid != null) or pre-aggregated pairs (pre_count != null) ->
+// per-partition utility-analysis metrics.
+struct PairsOut {  // pdp_preaggregate: stop after the pairs and export them
+  int64_t *pk, *count, *n_partitions;
+  double* sum;
+  int64_t* num_pairs;
+};
+
+int analysis_impl(pdp_ctx* ctx, const int64_t* pid, const int64_t* pk, const double* val, const int64_t* pre_count,
+                  const int64_t* pre_npart, int64_t n, int64_t U, int64_t P, int64_t num_sampled, int32_t metrics,
+                  const pdp_analysis_config* cfgs, int nconf, const pdp_analysis_outputs* out, void* workspace,
+                  size_t workspace_bytes, hipStream_t stream, const PairsOut* pairs_out = nullptr) {
+  if (!ctx || !cfgs || !out || (!out->metrics && !pairs_out)) return fail(PDP_ERR_INVALID_ARG, "null argument");
+  if (nconf < 1) return fail(PDP_ERR_INVALID_ARG, "num_configs must be >= 1");
+  if (P < 1 || P > (1ll << 31) - 2) return fail(PDP_ERR_INVALID_ARG, "num_partitions must be in [1, 2^31 - 2]");
+  if (U < 1 || U > (1ll << 32) - 2) return fail(PDP_ERR_INVALID_ARG, "num_privacy_ids must be in [1, 2^32 - 2]");
+  if (n < 0 || n >= (1ll << 32)) return fail(PDP_ERR_INVALID_ARG, "num_rows must be in [0, 2^32)");
+  const int mflags = metrics & (PDP_METRIC_SUM | PDP_METRIC_COUNT | PDP_METRIC_PRIVACY_ID_COUNT);
+  if (mflags == 0 || mflags != metrics)
+    return fail(PDP_ERR_INVALID_ARG, "utility analysis supports COUNT, SUM and PRIVACY_ID_COUNT");
+  if (n > 0 && (!pk || (!pid && !pre_count))) return fail(PDP_ERR_INVALID_ARG, "columns required");
+  if ((mflags & PDP_METRIC_SUM) && n > 0 && !val) return fail(PDP_ERR_INVALID_ARG, "value column required for SUM");
+  if (num_sampled < 0 || num_sampled > P) num_sampled = P;
+  AnaLayout L;
+  if (int rc = ana_layout(n, U, P, cfgs, nconf, L)) return rc;
+  const bool priv = cfgs[0].selection != PDP_SELECTION_NONE;
+  if (priv && !out->prob_keep) return fail(PDP_ERR_INVALID_ARG, "prob_keep output required for private selection");
+  if (!workspace || workspace_bytes < L.total) return fail(PDP_ERR_WORKSPACE, "workspace too small");
+  DeviceGuard dg(ctx->device);
+  if (!dg.ok) return fail(PDP_ERR_HIP, "hipSetDevice failed");
+  char* ws = (char*)workspace;
+  Rec* ra = (Rec*)(ws + L.recs_a);
+  Rec* rb = (Rec*)(ws + L.recs_b);
+  long long* flags = (long long*)(ws + L.flags);
+  uint32_t* ppk = (uint32_t*)(ws + L.ppk);
+  uint32_t* pref = (uint32_t*)(ws + L.pref);
+  uint32_t* pcnt = (uint32_t*)(ws + L.pcnt);
+  double* psum = (double*)(ws + L.psum);
+  uint32_t* npart = (uint32_t*)(ws + L.npart);
+  int64_t* pbeg = (int64_t*)(ws + L.pbeg);
+  double* mom = priv ? (double*)(ws + L.mom) : nullptr;
+  AnaCfg* dcfg = (AnaCfg*)(ws + L.cfg);
+  double* dkeep = (double*)(ws + L.keep);
+  unsigned long long* hist = (unsigned long long*)(ws + L.hist);
+  unsigned long long* off = (unsigned long long*)(ws + L.off);
+  unsigned long long* counters = (unsigned long long*)(ws + L.counters);
+  unsigned long long* status = (unsigned long long*)(ws + L.status);
+  for (AnaCfg& g : L.cfgs) g.keep = dkeep + (uintptr_t)g.keep;
+  HIP_TRY(hipMemcpyAsync(dcfg, L.cfgs.data(), L.cfgs.size() * sizeof(AnaCfg), hipMemcpyHostToDevice, stream));
+  if (!L.keep_all.empty())
+    HIP_TRY(hipMemcpyAsync(dkeep, L.keep_all.data(), L.keep_all.size() * 8, hipMemcpyHostToDevice, stream));
+  HIP_TRY(hipMemsetAsync(ws + L.hist, 0, L.status - L.hist, stream));  // hist, off, counters
+  HIP_TRY(hipMemsetAsync(npart, 0, (size_t)U * 4, stream));
+  const int nb = ((mflags & PDP_METRIC_SUM) != 0) + ((mflags & PDP_METRIC_COUNT) != 0) +
+                 ((mflags & PDP_METRIC_PRIVACY_ID_COUNT) != 0);
+  if (out->metrics) HIP_TRY(hipMemsetAsync(out->metrics, 0, (size_t)nconf * nb * 5 * P * 8, stream));
+  if (mom) HIP_TRY(hipMemsetAsync(mom, 0, (size_t)nconf * 4 * P * 8, stream));
+  ctx->tile_slot = kCtrTile0;
+  ctx->stats = pdp_stats{};
+  const size_t status_bytes = (size_t)L.tiles * kStatusStride * 8;
+  const int pkbits = std::max(1, pdp::ceil_log2_u64((uint64_t)P + 1));
+  int64_t M = 0;
+  if (n > 0) {
+    ProfScope ps(ctx, PDP_STAGE_ANALYSIS_PAIRS, stream);
+    const int g = grid_for(n, kThreads, 8192);
+    Rec* sorted = nullptr;
+    if (pid) {
+      // rows -> (pk, pid)-sorted records -> pairs
+      hipLaunchKernelGGL(k_ana_pack, dim3(g), dim3(kThreads), 0, stream, pid, pk, val, n, U, P, ra, counters);
+      const int pidbits = std::max(1, pdp::ceil_log2_u64((uint64_t)U + 1));
+      KeySpec ks = composite_spec(1, pkbits, pidbits, pidbits, (uint32_t)std::min<int64_t>(U, 0xFFFFFFFFll),
+                                  (uint32_t)P);
+      if (int rc = sort_recs(ctx, ra, rb, n, ks, hist, off, counters, status, status_bytes, workspace, stream, &sorted))
+        return rc;
+      hipLaunchKernelGGL(k_ana_group_flags, dim3(g), dim3(kThreads), 0, stream, sorted, n, flags);
+      if (int rc = scan_inplace(flags, n, stream)) return rc;
+      hipLaunchKernelGGL(k_ana_pairs, dim3(g), dim3(kThreads), 0, stream, sorted, n, flags, num_sampled, ppk, pref,
+                         pcnt, psum, npart);
+      hipLaunchKernelGGL(k_ana_count_pairs, dim3(1), dim3(1), 0, stream, sorted, n, flags, num_sampled, counters);
+    } else {
+      // pre-aggregated pairs -> sorted by pk
+      hipLaunchKernelGGL(k_ana_pack_pre, dim3(g), dim3(kThreads), 0, stream, pk, val, n, P, ra, counters);
+      KeySpec ks{};
+      ks.mode = 0;
+      ks.num_pids = 0xFFFFFFFFu;
+      ks.num_parts = (uint32_t)P;
+      for (int sh = 0; sh < pkbits; sh += 8) {
+        ks.shift[ks.passes] = sh;
+        ks.bits[ks.passes] = std::min(8, pkbits - sh);
+        ++ks.passes;
+      }
+      if (int rc = sort_recs(ctx, ra, rb, n, ks, hist, off, counters, status, status_bytes, workspace, stream, &sorted))
+        return rc;
+      hipLaunchKernelGGL(k_ana_pairs_pre, dim3(g), dim3(kThreads), 0, stream, sorted, n, pre_count, pre_npart, ppk,
+                         pref, pcnt, psum, npart);
+    }
+    HIP_TRY(hipGetLastError());
+    unsigned long long host_ctr[kCtrAnaPairs + 1];
+    HIP_TRY(hipMemcpyAsync(host_ctr, counters, sizeof(host_ctr), hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipStreamSynchronize(stream));
+    if (host_ctr[kCtrErr]) return fail(PDP_ERR_INTERNAL, "radix look-back timed out");
+    if (host_ctr[kCtrInvalid]) return fail(PDP_ERR_OUT_OF_RANGE, "privacy id or partition id out of range");
+    M = (int64_t)host_ctr[kCtrAnaPairs];
+  }
+  ctx->stats.kept_rows_in = M;  // pairs of sampled partitions
+  if (pairs_out) {
+    *pairs_out->num_pairs = M;
+    if (M > 0)
+      hipLaunchKernelGGL(k_ana_export, dim3(grid_for(M, kThreads, 8192)), dim3(kThreads), 0, stream, ppk, pref, pcnt,
+                         psum, npart, M, pairs_out->pk, pairs_out->count, pairs_out->sum, pairs_out->n_partitions);
+    HIP_TRY(hipGetLastError());
+    return 0;
+  }
+  ProfScope ps(ctx, PDP_STAGE_ANALYSIS_METRICS, stream);
+  const AnaCfg* cfg_d = dcfg;
+  hipLaunchKernelGGL(k_ana_bounds, dim3(grid_for(P + 1, kThreads, 8192)), dim3(kThreads), 0, stream, ppk, M, P, pbeg);
+  if (out->privacy_ids)
+    hipLaunchKernelGGL(k_ana_pid_counts, dim3(grid_for(P, kThreads, 8192)), dim3(kThreads), 0, stream, pbeg, P,
+                       out->privacy_ids);
+  if (!priv)
+    hipLaunchKernelGGL(k_ana_public_init, dim3(grid_for((int64_t)nconf * P, kThreads, 8192)), dim3(kThreads), 0, stream,
+                       cfg_d, nconf, mflags, P, out->metrics);
+  const unsigned cgroups = (unsigned)((nconf + 63) / 64);
+  if (M > 0) {
+    const int64_t waves = (M + kAnaChunk - 1) / kAnaChunk;
+    hipLaunchKernelGGL(k_ana_metrics, dim3((unsigned)((waves + 3) / 4), cgroups), dim3(256), 0, stream, ppk, pref,
+                       pcnt, psum, npart, M, cfg_d, nconf, mflags, P, out->metrics, mom);
+  }
+  if (priv) {
+    const int64_t blocks = std::min<int64_t>((P + kAnaSelWaves - 1) / kAnaSelWaves, 16384);
+    hipLaunchKernelGGL(k_ana_select, dim3((unsigned)blocks, cgroups), dim3(64 * kAnaSelWaves), 0, stream, pref, npart,
+                       pbeg, P, cfg_d, nconf, (const double*)mom, out->prob_keep);
+  }
+  HIP_TRY(hipGetLastError());
+  return 0;
+}
+
 }  // namespace
 
 int pdp_bound_accumulate(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp,
@@ -2130,6 +2359,56 @@ int pdp_profile_read(pdp_ctx* ctx, double* ms_out, int64_t* launches_out, int re
     }
   }
   return 0;
+}
+
+int pdp_analysis_workspace_size(int64_t num_rows, int64_t num_privacy_ids, int64_t num_partitions,
+                                const pdp_analysis_config* cfgs, int32_t num_configs, size_t* bytes) {
+  if (!cfgs || !bytes || num_rows < 0 || num_partitions < 1 || num_configs < 1)
+    return fail(PDP_ERR_INVALID_ARG, "bad analysis workspace args");
+  AnaLayout L;
+  if (int rc = ana_layout(num_rows, std::max<int64_t>(num_privacy_ids, 1), num_partitions, cfgs, num_configs, L))
+    return rc;
+  *bytes = L.total;
+  return 0;
+}
+
+int pdp_utility_analysis(pdp_ctx* ctx, const pdp_columns* cols, int64_t num_sampled_partitions, int32_t metrics,
+                         const pdp_analysis_config* cfgs, int32_t num_configs, const pdp_analysis_outputs* out,
+                         void* workspace, size_t workspace_bytes, void* stream) {
+  if (!cols) return fail(PDP_ERR_INVALID_ARG, "null argument");
+  if (cols->num_rows > 0 && !cols->pid) return fail(PDP_ERR_INVALID_ARG, "pid column required");
+  return analysis_impl(ctx, cols->pid, cols->pk, cols->value, nullptr, nullptr, cols->num_rows,
+                       cols->num_privacy_ids, cols->num_partitions, num_sampled_partitions, metrics, cfgs, num_configs,
+                       out, workspace, workspace_bytes, (hipStream_t)stream);
+}
+
+int pdp_utility_analysis_preaggregated(pdp_ctx* ctx, const int64_t* pk, const int64_t* count, const double* sum,
+                                       const int64_t* n_partitions, int64_t num_pairs, int64_t num_partitions,
+                                       int32_t metrics, const pdp_analysis_config* cfgs, int32_t num_configs,
+                                       const pdp_analysis_outputs* out, void* workspace, size_t workspace_bytes,
+                                       void* stream) {
+  if (num_pairs > 0 && (!count || !n_partitions)) return fail(PDP_ERR_INVALID_ARG, "count / n_partitions required");
+  return analysis_impl(ctx, nullptr, pk, sum, count, n_partitions, num_pairs, std::max<int64_t>(num_pairs, 1),
+                       num_partitions, num_partitions, metrics, cfgs, num_configs, out, workspace, workspace_bytes,
+                       (hipStream_t)stream);
+}
+
+int pdp_preaggregate(pdp_ctx* ctx, const pdp_columns* cols, int64_t num_sampled_partitions, int64_t* out_pk,
+                     int64_t* out_count, double* out_sum, int64_t* out_n_partitions, int64_t* num_pairs,
+                     void* workspace, size_t workspace_bytes, void* stream) {
+  if (!cols || !num_pairs) return fail(PDP_ERR_INVALID_ARG, "null argument");
+  if (cols->num_rows > 0 && (!cols->pid || !out_pk || !out_count || !out_sum || !out_n_partitions))
+    return fail(PDP_ERR_INVALID_ARG, "pid column and outputs required");
+  *num_pairs = 0;
+  pdp_analysis_config cfg{};
+  cfg.max_partitions_contributed = 1;
+  cfg.max_contributions_per_partition = 1;
+  pdp_analysis_outputs none{};
+  const PairsOut po{out_pk, out_count, out_n_partitions, out_sum, num_pairs};
+  return analysis_impl(ctx, cols->pid, cols->pk, cols->value, nullptr, nullptr, cols->num_rows,
+                       cols->num_privacy_ids, cols->num_partitions, num_sampled_partitions,
+                       cols->value ? PDP_METRIC_SUM | PDP_METRIC_COUNT : PDP_METRIC_COUNT, &cfg, 1, &none, workspace,
+                       workspace_bytes, (hipStream_t)stream, &po);
 }
 
 int pdp_shard_workspace_size(int64_t num_rows, int32_t world_size, size_t* bytes) {

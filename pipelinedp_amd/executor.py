@@ -185,6 +185,73 @@ class HipExecutor:
                                           ctypes.byref(outs), self.stream_handle), "pdp_release")
         return keep[:P], out[:, :P], fields
 
+    def _analysis_outputs(self, cfgs, num_partitions, metrics_mask, private):
+        torch = self.torch
+        nb = bin(metrics_mask & (native.METRIC_SUM | native.METRIC_COUNT | native.METRIC_PRIVACY_ID_COUNT)).count("1")
+        P = int(num_partitions)
+        metrics = torch.empty((len(cfgs), nb, 5, P), dtype=torch.float64, device=self.device)
+        prob = torch.empty((len(cfgs), P), dtype=torch.float64, device=self.device) if private else None
+        pids = torch.empty(P, dtype=torch.int64, device=self.device)
+        return metrics, prob, pids, native.AnalysisOutputs(_ptr(metrics), _ptr(prob), _ptr(pids))
+
+    def analyze(self, pid, pk, value, num_privacy_ids: int, num_partitions: int, metrics_mask: int,
+                cfgs: Sequence["native.AnalysisConfig"], num_sampled_partitions: Optional[int] = None,
+                pre_count=None, pre_n_partitions=None):
+        """pdp_utility_analysis (raw rows) or, with pre_count / pre_n_partitions,
+        pdp_utility_analysis_preaggregated (pk = pair partitions, value = pair
+        sums) -> (metrics [C, nb, 5, P], prob_keep [C, P] or None, privacy ids
+        with data per partition [P])."""
+        k = len(cfgs)
+        carr = (native.AnalysisConfig * k)(*cfgs)
+        private = cfgs[0].selection != native.SELECTION_NONE
+        n = int(pk.numel())
+        P = int(num_partitions)
+        pre = pre_count is not None
+        U = n if pre else int(max(num_privacy_ids, 1))
+        nbytes = ctypes.c_size_t(0)
+        native.check(self.lib.pdp_analysis_workspace_size(n, U, P, carr, k, ctypes.byref(nbytes)),
+                     "pdp_analysis_workspace_size")
+        ws = self._workspace(nbytes.value)
+        metrics, prob, pids, outs = self._analysis_outputs(cfgs, P, metrics_mask, private)
+        if pre:
+            native.check(self.lib.pdp_utility_analysis_preaggregated(
+                self.ctx, _ptr(pk), _ptr(pre_count), _ptr(value), _ptr(pre_n_partitions), n, P, metrics_mask, carr, k,
+                ctypes.byref(outs), ctypes.c_void_p(ws.data_ptr()), ws.numel(), self.stream_handle),
+                "pdp_utility_analysis_preaggregated")
+        else:
+            cols = self._columns(pid, pk, value, U, P)
+            ns = P if num_sampled_partitions is None else int(num_sampled_partitions)
+            native.check(self.lib.pdp_utility_analysis(self.ctx, ctypes.byref(cols), ns, metrics_mask, carr, k,
+                                                       ctypes.byref(outs), ctypes.c_void_p(ws.data_ptr()), ws.numel(),
+                                                       self.stream_handle), "pdp_utility_analysis")
+        return metrics, prob, pids
+
+    def preaggregate(self, pid, pk, value, num_privacy_ids: int, num_partitions: int,
+                     num_sampled_partitions: Optional[int] = None):
+        """pdp_preaggregate -> (pk, count, sum, n_partitions) device tensors, one
+        per (privacy id, sampled partition) pair."""
+        torch = self.torch
+        n = int(pk.numel())
+        P = int(num_partitions)
+        cols = self._columns(pid, pk, value, num_privacy_ids, P)
+        cfg = native.AnalysisConfig(1, 1, 0.0, 0.0, 0, 0, 0.0, 0.0)
+        nbytes = ctypes.c_size_t(0)
+        native.check(self.lib.pdp_analysis_workspace_size(n, int(max(num_privacy_ids, 1)), P, ctypes.byref(cfg), 1,
+                                                          ctypes.byref(nbytes)), "pdp_analysis_workspace_size")
+        ws = self._workspace(nbytes.value)
+        m = max(n, 1)
+        opk = torch.empty(m, dtype=torch.int64, device=self.device)
+        ocnt = torch.empty(m, dtype=torch.int64, device=self.device)
+        osum = torch.empty(m, dtype=torch.float64, device=self.device)
+        onp = torch.empty(m, dtype=torch.int64, device=self.device)
+        cnt = ctypes.c_int64(0)
+        ns = P if num_sampled_partitions is None else int(num_sampled_partitions)
+        native.check(self.lib.pdp_preaggregate(self.ctx, ctypes.byref(cols), ns, _ptr(opk), _ptr(ocnt), _ptr(osum),
+                                               _ptr(onp), ctypes.byref(cnt), ctypes.c_void_p(ws.data_ptr()),
+                                               ws.numel(), self.stream_handle), "pdp_preaggregate")
+        k = cnt.value
+        return opk[:k], ocnt[:k], osum[:k], onp[:k]
+
     def shard_rows(self, pid, pk, value, world_size: int):
         """pdp_shard_rows: rows grouped by destination rank shard_of(pid)
         (stable) -> (pid, pk, value, rows_per_rank list)."""

@@ -54,6 +54,16 @@ class Outputs(ctypes.Structure):
     _fields_ = [("keep", c_vp), ("metrics", c_vp)]
 
 
+class AnalysisConfig(ctypes.Structure):
+    _fields_ = [("max_partitions_contributed", c_i64), ("max_contributions_per_partition", c_i64),
+                ("min_sum_per_partition", c_f64), ("max_sum_per_partition", c_f64),
+                ("selection", c_i32), ("reserved", c_i32), ("selection_eps", c_f64), ("selection_delta", c_f64)]
+
+
+class AnalysisOutputs(ctypes.Structure):
+    _fields_ = [("metrics", c_vp), ("prob_keep", c_vp), ("privacy_ids", c_vp)]
+
+
 class Stats(ctypes.Structure):
     _fields_ = [("kept_rows_in", c_i64), ("fallback_rows", c_i64), ("fallback_ranges", c_i64),
                 ("sort_passes", c_i32), ("bucket_low_bits", c_i32), ("sweep_cycles", c_i64 * 4),
@@ -81,6 +91,15 @@ SIGNATURES = [
                                               ctypes.POINTER(c_i64)]),
     ("pdp_selection_threshold", c_i32, [c_i32, c_f64, c_f64, c_i64, ctypes.POINTER(c_f64),
                                         ctypes.POINTER(c_f64)]),
+    ("pdp_analysis_workspace_size", c_i32, [c_i64, c_i64, c_i64, ctypes.POINTER(AnalysisConfig), c_i32,
+                                            ctypes.POINTER(ctypes.c_size_t)]),
+    ("pdp_utility_analysis", c_i32, [c_vp, ctypes.POINTER(Columns), c_i64, c_i32, ctypes.POINTER(AnalysisConfig),
+                                     c_i32, ctypes.POINTER(AnalysisOutputs), c_vp, ctypes.c_size_t, c_vp]),
+    ("pdp_utility_analysis_preaggregated", c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i32,
+                                                   ctypes.POINTER(AnalysisConfig), c_i32,
+                                                   ctypes.POINTER(AnalysisOutputs), c_vp, ctypes.c_size_t, c_vp]),
+    ("pdp_preaggregate", c_i32, [c_vp, ctypes.POINTER(Columns), c_i64, c_vp, c_vp, c_vp, c_vp, ctypes.POINTER(c_i64),
+                                 c_vp, ctypes.c_size_t, c_vp]),
     ("pdp_shard_workspace_size", c_i32, [c_i64, c_i32, ctypes.POINTER(ctypes.c_size_t)]),
     ("pdp_shard_rows", c_i32, [c_vp, ctypes.POINTER(Columns), c_i32, c_vp, c_vp, c_vp, ctypes.POINTER(c_i64), c_vp,
                                ctypes.c_size_t, c_vp]),
@@ -92,7 +111,7 @@ SIGNATURES = [
 ]
 
 STAGES = ["histogram", "onesweep_first", "onesweep_rest", "buckets", "generic", "release", "enforced",
-          "tile_counts"]
+          "tile_counts", "analysis_pairs", "analysis_metrics"]
 
 _lib = None
 

@@ -84,3 +84,29 @@ class CpuExecutor:
         counts = np.bincount(dest, minlength=world_size).tolist()
         take = lambda t: None if t is None else torch.from_numpy(np.ascontiguousarray(t.numpy()[order]))  # noqa
         return take(pid), take(pk), take(value), counts
+
+    # -- utility analysis (pdp_utility_analysis restated) -------------------
+    def analyze(self, pid, pk, value, num_privacy_ids, num_partitions, metrics_mask, cfgs,
+                num_sampled_partitions=None, pre_count=None, pre_n_partitions=None):
+        import pdp_analysis_oracle as ao
+        torch = self.torch
+        P = int(num_partitions)
+        sel = {native.SELECTION_NONE: None, **_SEL}
+        ocfgs = [ao.AnalysisConfig(c.max_partitions_contributed, c.max_contributions_per_partition,
+                                   c.min_sum_per_partition, c.max_sum_per_partition, sel[c.selection],
+                                   c.selection_eps, c.selection_delta) for c in cfgs]
+        public = ocfgs[0].selection is None
+        if pre_count is not None:
+            ppk = pk.numpy()
+            keep = (ppk >= 0) & (ppk < P)
+            pairs = (ppk[keep], pre_count.numpy()[keep], value.numpy()[keep], pre_n_partitions.numpy()[keep])
+        else:
+            pairs = ao.preaggregate(pid.numpy(), pk.numpy(), None if value is None else value.numpy(),
+                                    num_sampled=num_sampled_partitions)
+        names = [m for m, bit in (("sum", native.METRIC_SUM), ("count", native.METRIC_COUNT),
+                                  ("privacy_id_count", native.METRIC_PRIVACY_ID_COUNT)) if metrics_mask & bit]
+        out = ao.per_partition(*pairs, P, ocfgs, names, public=public)
+        metrics = np.stack([np.stack([out[m][c] for m in names]) for c in range(len(ocfgs))])
+        prob = None if public else torch.from_numpy(out["prob_keep"])
+        pids = np.bincount(pairs[0], minlength=P).astype(np.int64)
+        return torch.from_numpy(metrics), prob, torch.from_numpy(pids)

@@ -1,67 +1,74 @@
-"""Bounding sweep host layer (pipelinedp_amd/analysis.py).
-
-CPU: MultiParameterConfiguration validation and parameter substitution, as
-the reference's analysis/tests/data_structures_test.py checks them.
-GPU: bounded_accumulators_sweep on Python rows equals, per configuration, the
-CPU oracle (oracle/pdp_oracle.py:bound_and_accumulate) with the same seed.
-"""
+"""Utility analysis (BASELINE configs[4]) on the CPU: the oracle restatement
+and the host engine (pipelinedp_amd.analysis, executor replaced by the CPU
+stand-in) against golden vectors from the reference UtilityAnalysisEngine,
+and the reference tests' own known answers
+(analysis/tests/utility_analysis_engine_test.py:157-220, 222-302)."""
 import numpy as np
 import pytest
 
-import pdp_oracle as o
-from pipelinedp_amd import AggregateParams, DataExtractors, Metrics
-from pipelinedp_amd.analysis import MultiParameterConfiguration, bounded_accumulators_sweep
+import pipelinedp_amd as pdp
+from analysis_util import CASES, check_case, run_case
+from pipelinedp_amd import analysis as A
 
 
-def _params():
-    return AggregateParams(metrics=[Metrics.COUNT, Metrics.SUM], max_partitions_contributed=1,
-                           max_contributions_per_partition=1, min_value=0.0, max_value=5.0)
+def _backend():
+    from cpu_executor import CpuExecutor
+    b = pdp.HipBackend()
+    b._executor = CpuExecutor()
+    return b
 
 
-def test_multi_config_validation():
-    with pytest.raises(ValueError, match="at least 1"):
-        MultiParameterConfiguration()
-    with pytest.raises(ValueError, match="same length"):
-        MultiParameterConfiguration(max_partitions_contributed=[1, 2], max_contributions_per_partition=[1])
-    with pytest.raises(ValueError, match="both set"):
-        MultiParameterConfiguration(min_sum_per_partition=[0.0])
+@pytest.mark.parametrize("name", CASES)
+def test_engine_matches_reference_golden_on_cpu_executor(name):
+    d, got = run_case(name, _backend())
+    check_case(d, got)
 
 
-def test_get_aggregate_params_substitutes_bounds():
-    m = MultiParameterConfiguration(max_partitions_contributed=[1, 2], max_contributions_per_partition=[10, 11])
-    assert m.size == 2
-    p = m.get_aggregate_params(_params(), 1)
-    assert (p.max_partitions_contributed, p.max_contributions_per_partition) == (2, 11)
-    assert p.min_value == 0.0 and p.metrics == [Metrics.COUNT, Metrics.SUM]
-    base = _params()
-    m.get_aggregate_params(base, 0)
-    assert base.max_partitions_contributed == 1  # the input is not modified
+def test_reference_per_partition_known_answers():
+    # analysis/tests/utility_analysis_engine_test.py:203-220
+    _, got = run_case("reference_per_partition_errors", _backend())
+    assert len(got) == 10
+    for _, v in got.items():
+        assert v[1].per_partition_error_max == -10
+        assert v[1].expected_cross_partition_error == pytest.approx(-18.0, abs=1e-5)
+        assert v[1].std_cross_partition_error == pytest.approx(1.89736, abs=1e-5)
+        assert v[1].std_noise == pytest.approx(11.95312, abs=1e-5)
 
 
-@pytest.mark.gpu
-def test_sweep_on_rows_matches_oracle():
-    n, U, P = 20000, 400, 300
-    pid, pk, val = o.synth_rows(n, U, P, seed=31, zipf_s=1.1)
-    rows = list(zip(pid.tolist(), pk.tolist(), (val * 0.7).tolist()))
-    ext = DataExtractors(privacy_id_extractor=lambda r: r[0], partition_extractor=lambda r: r[1],
-                         value_extractor=lambda r: r[2])
-    multi = MultiParameterConfiguration(max_partitions_contributed=[1, 3, 8],
-                                        max_contributions_per_partition=[1, 2, 5])
-    res = bounded_accumulators_sweep(rows, _params(), ext, multi, sampling_seed=50)
-    assert len(res) == 3
-    # encode_rows numbers pids and partitions in first-appearance order
-    pid_order = {p: i for i, p in enumerate(dict.fromkeys(pid.tolist()))}
-    pk_order = {k: i for i, k in enumerate(dict.fromkeys(pk.tolist()))}
-    pid_dense = np.array([pid_order[p] for p in pid.tolist()])
-    pk_dense = np.array([pk_order[k] for k in pk.tolist()])
-    keys = list(pk_order)
-    for i, got in enumerate(res):
-        bp = o.BoundParams(multi.max_partitions_contributed[i], multi.max_contributions_per_partition[i], 0.0, 5.0)
-        ref = o.bound_and_accumulate(pid_dense, pk_dense, val * 0.7, len(keys), bp, "hash", seed=50 + i)
-        for j, key in enumerate(keys):
-            if ref.row_count[j] == 0:
-                assert key not in got
-                continue
-            a = got[key]
-            assert (a.privacy_id_count, a.count) == (int(ref.row_count[j]), int(ref.count[j]))
-            assert abs(a.sum - ref.sum[j]) <= 1e-9 * (abs(ref.sum[j]) + 1)
+def test_reference_multi_parameters_known_answers():
+    # analysis/tests/utility_analysis_engine_test.py:264-302 (public partitions, 2 configurations)
+    _, got = run_case("reference_multi_parameters", _backend())
+    G = pdp.NoiseKind.GAUSSIAN
+    assert got[0] == (A.SumMetrics(1.0, 0.0, 0.0, -0.5, 0.5, 5.87109375, G),
+                      A.SumMetrics(1.0, 0.0, 0.0, 0, 0.0, pytest.approx(16.60596081442783), G))
+    assert got[1] == (A.SumMetrics(2.0, 0.0, -1.0, -0.5, 0.5, 5.87109375, G),
+                      A.SumMetrics(2.0, 0.0, 0.0, 0, 0.0, pytest.approx(16.60596081442783), G))
+
+
+def test_analysis_validation_errors():
+    params = pdp.AggregateParams(metrics=[pdp.Metrics.MEAN], max_partitions_contributed=1,
+                                 max_contributions_per_partition=1, min_value=0, max_value=1)
+    eng = A.UtilityAnalysisEngine(pdp.NaiveBudgetAccountant(1, 1e-6), _backend())
+    ex = pdp.DataExtractors(privacy_id_extractor=lambda r: r, partition_extractor=lambda r: r,
+                            value_extractor=lambda r: r)
+    with pytest.raises(NotImplementedError, match="unsupported metric"):
+        eng.analyze([1], A.UtilityAnalysisOptions(1, 1e-6, params), ex)
+    count = pdp.AggregateParams(metrics=[pdp.Metrics.COUNT], max_partitions_contributed=1,
+                                max_contributions_per_partition=1)
+    with pytest.raises(ValueError, match="PreAggregateExtractors"):
+        eng.analyze([1], A.UtilityAnalysisOptions(1, 1e-6, count, pre_aggregated_data=True), ex)
+    with pytest.raises(ValueError, match="can't be called"):
+        eng.aggregate([1], count, ex)
+    with pytest.raises(ValueError):
+        A.UtilityAnalysisOptions(1, 1e-6, count, partitions_sampling_prob=0)
+    with pytest.raises(ValueError):
+        A.MultiParameterConfiguration(max_partitions_contributed=[1, 2], max_contributions_per_partition=[1])
+
+
+def test_value_sampler_matches_reference_counts():
+    # tests/sampling_utils_test.py:54-79 pins ValueSampler on range(1000)
+    from golden_util import known_answers
+    for c in known_answers()["value_sampler"]:
+        s = A.ValueSampler(c["rate"])
+        vals = [str(v) for v in range(c["n"])] if c["str"] else range(c["n"])
+        assert sum(s.keep(v) for v in vals) == c["kept"]

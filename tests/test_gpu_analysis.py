@@ -1,0 +1,104 @@
+"""Utility analysis on the MI355X (pdp_utility_analysis through the C ABI and
+the host engine) against the reference UtilityAnalysisEngine goldens, the
+reference tests' known answers (analysis/tests/utility_analysis_engine_test.py:
+157-220, 222-302) and the numpy oracle on random multi-configuration inputs.
+
+Tolerances: fp64 sums 1e-9 relative (summation order); keep probabilities
+1e-9 relative (the Poisson-binomial recurrence runs in the same order as the
+reference's, pdp_analysis.inc: k_ana_select)."""
+import numpy as np
+import pytest
+
+import pdp_analysis_oracle as ao
+import pdp_oracle as o
+from analysis_util import CASES, check_case, run_case
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ex():
+    from pipelinedp_amd.executor import HipExecutor
+    return HipExecutor(0)
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_gpu_engine_matches_reference_golden(name):
+    import pipelinedp_amd as pdp
+    d, got = run_case(name, pdp.HipBackend())
+    check_case(d, got)
+
+
+def test_gpu_reference_known_answers():
+    import pipelinedp_amd as pdp
+    _, got = run_case("reference_per_partition_errors", pdp.HipBackend())
+    assert len(got) == 10
+    for v in got.values():
+        assert v[1].per_partition_error_max == -10
+        assert v[1].expected_cross_partition_error == pytest.approx(-18.0, abs=1e-5)
+        assert v[1].std_cross_partition_error == pytest.approx(1.89736, abs=1e-5)
+        assert v[1].std_noise == pytest.approx(11.95312, abs=1e-5)
+
+
+def _cfgs(rng, C, private):
+    from pipelinedp_amd import native
+    sel = [native.SELECTION_TRUNCATED_GEOMETRIC, native.SELECTION_LAPLACE, native.SELECTION_GAUSSIAN]
+    out = []
+    for c in range(C):
+        a = native.AnalysisConfig()
+        a.max_partitions_contributed = int(rng.integers(1, 40))
+        a.max_contributions_per_partition = int(rng.integers(1, 6))
+        a.min_sum_per_partition = float(rng.uniform(-5, 1))
+        a.max_sum_per_partition = float(a.min_sum_per_partition + rng.uniform(0.1, 8))
+        if private:
+            a.selection = sel[c % 3]
+            a.selection_eps, a.selection_delta = 1.0, 1e-5
+        out.append(a)
+    return out
+
+
+@pytest.mark.parametrize("private", [True, False])
+@pytest.mark.parametrize("C", [1, 64, 70])
+def test_analysis_matches_oracle_many_configs(ex, private, C):
+    import torch
+    from pipelinedp_amd import native
+    rng = np.random.default_rng(C + 100 * private)
+    n, U, P = 40000, 1500, 400
+    pid, pk, val = o.synth_rows(n, U, P, seed=C, zipf_s=1.1)
+    if not private:
+        pk = np.where(pk % 7 == 3, -1, pk)  # non-public rows
+    cfgs = _cfgs(rng, C, private)
+    mask = native.METRIC_SUM | native.METRIC_COUNT | native.METRIC_PRIVACY_ID_COUNT
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
+    metrics, prob, pids = ex.analyze(t(pid), t(pk), t(val), U, P, mask, cfgs)
+    torch.cuda.synchronize()
+    pairs = ao.preaggregate(pid, pk, val)
+    sel = {0: None, 1: "truncated_geometric", 2: "laplace", 3: "gaussian"}
+    ocfgs = [ao.AnalysisConfig(c.max_partitions_contributed, c.max_contributions_per_partition,
+                               c.min_sum_per_partition, c.max_sum_per_partition, sel[c.selection], c.selection_eps,
+                               c.selection_delta) for c in cfgs]
+    ref = ao.per_partition(*pairs, P, ocfgs, ["sum", "count", "privacy_id_count"], public=not private)
+    m = metrics.cpu().numpy()
+    for b, name in enumerate(["sum", "count", "privacy_id_count"]):
+        np.testing.assert_allclose(m[:, b], ref[name], rtol=1e-9, atol=1e-8, err_msg=name)
+    np.testing.assert_array_equal(pids.cpu().numpy(), np.bincount(pairs[0], minlength=P))
+    if private:
+        np.testing.assert_allclose(prob.cpu().numpy(), ref["prob_keep"], rtol=1e-9, atol=1e-12)
+        assert (pids.cpu().numpy() > 100).any() and ((pids.cpu().numpy() > 0) & (pids.cpu().numpy() <= 100)).any()
+
+
+def test_preaggregate_matches_oracle(ex):
+    import torch
+    n, U, P = 30000, 900, 300
+    pid, pk, val = o.synth_rows(n, U, P, seed=5, zipf_s=1.1)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
+    for ns in (P, 120):
+        gpk, gc, gs, gn = (a.cpu().numpy() for a in ex.preaggregate(t(pid), t(pk), t(val), U, P, ns))
+        rpk, rc, rs, rn = ao.preaggregate(pid, pk, val, num_sampled=ns)
+        key_g = np.lexsort((gc, gn, gpk))
+        key_r = np.lexsort((rc, rn, rpk))
+        np.testing.assert_array_equal(gpk[key_g], rpk[key_r])
+        np.testing.assert_array_equal(gc[key_g], rc[key_r])
+        np.testing.assert_array_equal(gn[key_g], rn[key_r])
+        np.testing.assert_allclose(np.sort(gs), np.sort(rs), rtol=1e-12, atol=1e-12)
+        assert gpk.max() < ns
