@@ -32,12 +32,21 @@ WORKLOADS = {
                cpu_sample=6e6),
     "c4": dict(rows=5e8, partitions=5e7, pids=1.25e7, zipf=1.1, l0=32, linf=4, public=False, metrics="mean",
                cpu_sample=5e5),  # the oracle's O(P) release dominates at P=5e7
-    # c5: utility-analysis sweep, COUNT under 64 bounding configs (L0 x Linf) over 1e8 rows;
-    # one sort by privacy id, then bounding + accumulation per config (pdp_bound_accumulate_sweep).
-    "c5": dict(rows=1e8, partitions=1e5, pids=1e6, zipf=1.1, l0=0, linf=0, public=True, metrics="count",
+    # c5: UtilityAnalysisEngine.analyze with 64 configurations (L0 x Linf) over 1e8 rows: per-partition
+    # COUNT / SUM / PRIVACY_ID_COUNT error metrics + truncated-geometric keep probability
+    # (pdp_utility_analysis); cpu_sample = total rows of the CPU baseline.
+    "c5": dict(rows=1e8, partitions=1e5, pids=1e6, zipf=1.1, l0=0, linf=0, public=False, metrics="analysis",
                cpu_sample=2e5),
 }
 SWEEP = [(l0, linf) for l0 in (1, 2, 4, 8, 16, 32, 64, 128) for linf in range(1, 9)]
+SWEEP_SUM_BOUNDS = (0.0, 20.0)  # min/max_sum_per_partition of every c5 configuration
+
+
+def analysis_oracle_cfgs(eps_sel=0.25, delta_sel=1e-6):
+    """c5 configurations for the CPU baseline (pdp_analysis_oracle)."""
+    import pdp_analysis_oracle as ao
+    lo, hi = SWEEP_SUM_BOUNDS
+    return [ao.AnalysisConfig(l0, linf, lo, hi, "truncated_geometric", eps_sel, delta_sel) for l0, linf in SWEEP]
 
 
 def parse():
@@ -73,6 +82,10 @@ def stage_bytes(stage, n_in, n_kept, P, nfields):
         "onesweep_rest": 32 * n_kept,  # read + write 16-B records
         "buckets": 16 * n_kept,  # read 16-B records once
         "release": P * (3 * 8 + 1 + 8 * nfields),
+        # c5: read the input columns once; read the (pk, privacy id, count, sum) pairs once and write
+        # C x P x (3 metrics x 5 + keep probability) doubles
+        "analysis_pairs": 24 * n_in,
+        "analysis_metrics": 20 * n_kept + P * len(SWEEP) * (5 * 3 + 1) * 8,
     }.get(stage)
 
 
@@ -136,6 +149,39 @@ def _cpu_bound(task):
     return idx, acc.row_count[idx], acc.count[idx], acc.sum[idx], acc.nsum[idx]
 
 
+def _cpu_analysis(task):
+    """Worker: per-partition metrics of a slice of the c5 configurations."""
+    import pdp_analysis_oracle as ao
+    lo, hi, P = task
+    ao.per_partition(*_SHM["pairs"], P, analysis_oracle_cfgs()[lo:hi], ["sum", "count", "privacy_id_count"])
+    return hi - lo
+
+
+def cpu_baseline_analysis(args, P, W):
+    """c5 on the host: oracle pre-aggregation of the sample, then the 64
+    configurations split over W processes (pdp_analysis_oracle.py)."""
+    import multiprocessing as mp
+
+    import pdp_analysis_oracle as ao
+    import pdp_oracle as o
+    m = int(args.cpu_sample)
+    U = max(1, int(args.pids * m / args.rows))
+    pid, pk, val = o.synth_rows(m, U, P, seed=args.seed, zipf_s=args.zipf)
+    t0 = time.perf_counter()
+    _SHM["pairs"] = ao.preaggregate(pid, pk, val)
+    ctx = mp.get_context("fork")
+    with ctx.Pool(W) as pool:
+        step = (len(SWEEP) + W - 1) // W
+        pool.map(_cpu_analysis, [(i, min(i + step, len(SWEEP)), P) for i in range(0, len(SWEEP), step)])
+    dt = time.perf_counter() - t0
+    del _SHM["pairs"]
+    return {"value": m / dt, "unit": "rows/s", "cores": W, "kind": "port", "plan_item": 3,
+            "host_cpus_visible": os.cpu_count(), "cpu_model": _cpu_model(),
+            "sample": f"c5: {m} rows, {U} privacy ids, {P} Zipf({args.zipf}) partitions, {len(SWEEP)} "
+                      f"configurations; numpy restatement (oracle/pdp_analysis_oracle.py): pre-aggregation on one "
+                      f"process, configurations split over {W}; {dt:.1f} s"}
+
+
 def cpu_baseline(args, P):
     """BASELINE.md CPU plan item 3: the numpy restatement (oracle/pdp_oracle.py)
     on the host cores of this box, privacy ids sharded over a process pool
@@ -154,6 +200,8 @@ def cpu_baseline(args, P):
     except AttributeError:
         cores = os.cpu_count() or 1
     W = max(1, min(16, cores))  # the GPU box's CPU share is 16 cores per GPU
+    if WORKLOADS[args.workload]["metrics"] == "analysis":
+        return cpu_baseline_analysis(args, P, W)
     m = int(args.cpu_sample) * W
     U = max(1, int(args.pids * m / args.rows))
     for name, dt in (("pid", np.int64), ("pk", np.int64), ("val", np.float64)):
@@ -243,12 +291,14 @@ def main():
     # lives on one rank (pid-sharded input, weak scaling); the sort uses the dense local ids.
     public = WORKLOADS[args.workload]["public"]
     count_sum = WORKLOADS[args.workload]["metrics"] == "count_sum"
-    sweep = WORKLOADS[args.workload]["metrics"] == "count"
+    sweep = WORKLOADS[args.workload]["metrics"] == "analysis"
     mask = native.METRIC_COUNT | native.METRIC_SUM | (0 if count_sum else native.METRIC_MEAN)
     if sweep:
-        mask = native.METRIC_COUNT
-        sweep_cfgs = [BoundConfig(mask, l0, linf, sampling_seed=args.seed + 1 + i) for i, (l0, linf) in
-                      enumerate(SWEEP)]
+        # UtilityAnalysisOptions(eps=1, delta=1e-6), metrics COUNT+SUM+PRIVACY_ID_COUNT, private selection:
+        # NaiveBudgetAccountant gives the GENERIC mechanism eps 1/4 and all of delta
+        mask = native.METRIC_COUNT | native.METRIC_SUM | native.METRIC_PRIVACY_ID_COUNT
+        ana_cfgs = [native.AnalysisConfig(l0, linf, SWEEP_SUM_BOUNDS[0], SWEEP_SUM_BOUNDS[1],
+                                          native.SELECTION_TRUNCATED_GEOMETRIC, 0, 0.25, 1e-6) for l0, linf in SWEEP]
     bounds = BoundConfig(mask, args.l0, args.linf, 0.0, 10.0, sampling_seed=args.seed + 1,
                          debug_flags=args.debug_flags)
     # NaiveBudgetAccountant(eps=1, delta=1e-6): MeanCombiner (Laplace) eps 0.5, selection eps 0.5 delta 1e-6
@@ -266,8 +316,8 @@ def main():
 
     def step():
         if sweep:
-            accs = ex.accumulate_sweep(pid, pk, val, U, P, sweep_cfgs)
-            return (accs[-1].row_count,)
+            metrics, prob, pids = ex.analyze(pid, pk, val, U, P, mask, ana_cfgs)
+            return (pids > 0,)
         if world is not None:
             return world.aggregate(ex, pid, pk, val, U, P, bounds, rel, gather=False)
         acc = ex.accumulate(pid, pk, val, U, P, bounds)
@@ -340,10 +390,11 @@ def main():
             "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f64",
             "data": "synthetic (on-device Philox generator, oracle/pdp_oracle.py:synth_rows)",
-            "config": {"workload": (f"c5: bounding sweep, COUNT under {len(SWEEP)} (L0, Linf) configs "
-                                    f"(L0 1..128 x Linf 1..8), {n:.2e} rows/GPU, {U:.1e} privacy ids, {P:.1e} "
-                                    f"Zipf({args.zipf}) partitions, one sort + {len(SWEEP)} bound/accumulate passes; "
-                                    f"value = input rows/s for the whole sweep") if sweep else
+            "config": {"workload": (f"c5: UtilityAnalysisEngine.analyze, {len(SWEEP)} configurations "
+                                    f"(L0 1..128 x Linf 1..8, sum bounds {SWEEP_SUM_BOUNDS}), COUNT+SUM+PRIVACY_ID_COUNT "
+                                    f"per-partition error metrics + truncated-geometric keep probability, "
+                                    f"{n:.2e} rows/GPU, {U:.1e} privacy ids, {P:.1e} Zipf({args.zipf}) partitions; "
+                                    f"value = input rows/s for the whole analysis") if sweep else
                                    f"{args.workload}: DP {'COUNT+SUM' if count_sum else 'COUNT+SUM+MEAN'}, "
                                    f"{n:.2e} rows/GPU, {U:.1e} privacy ids/GPU, {P:.1e} "
                                    f"{'public uniform' if public else f'Zipf({args.zipf})'} partitions, "

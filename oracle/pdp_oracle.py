@@ -35,6 +35,7 @@ DESIGN.md "Randomness"):
     that grid, and the released value is snapped to it (granularity
     snapping as in PyDP's secure mechanisms; not PyDP's implementation).
 """
+import functools
 import math
 from dataclasses import dataclass, field
 from typing import Dict, Optional
@@ -327,6 +328,7 @@ def adjusted_delta(delta, k):
     return -math.expm1(math.log1p(-delta) / k)
 
 
+@functools.lru_cache(maxsize=256)
 def truncated_geometric_table(eps, delta, max_partitions, max_len=1 << 22):
     """Keep probability p(n) of PyDP's truncated-geometric partition
     selection, n = 0..len-1; p(n) = 1 for n beyond the table.
@@ -349,7 +351,9 @@ def truncated_geometric_table(eps, delta, max_partitions, max_len=1 << 22):
             raise ValueError("truncated geometric table too long (eps too small)")
         if nxt <= prev:  # delta == 0 and eps tiny: never reaches 1
             raise ValueError("truncated geometric selection cannot keep partitions")
-    return np.asarray(p, dtype=np.float64)
+    t = np.asarray(p, dtype=np.float64)
+    t.flags.writeable = False  # cached: shared by every caller
+    return t
 
 
 def truncated_geometric_keep_prob(n, eps, delta, max_partitions):

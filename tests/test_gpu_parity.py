@@ -74,10 +74,16 @@ CONFIGS = [
     (30000, 250, 20000, 0.0, 65, 3, (0.0, 10.0), None, 1 | 2),  # L0 > 64: lean with two output slots per lane
     (30000, 200, 20000, 0.0, 128, 2, (0.0, 10.0), None, 1 | 4 | 16),  # largest L0 of the lean kernel
     (30000, 200, 20000, 0.0, 129, 2, (0.0, 10.0), None, 1 | 2 | 16),  # L0 > 128: batch kernel
+    (40000, 400, 40, 1.1, 8, 2, (0.0, 10.0), None, 1 | 2 | 4 | 16),  # sorted K2 + second (L_inf) sort
+    (20000, 400, 12, 0.0, 9, 3, (-1.0, 4.0), None, 1 | 4 | 8),  # sorted K2, every group over L_inf
+    (12000, 200, 500, 1.1, 70, 1, (0.0, 10.0), None, 1 | 2 | 16),  # sorted K2 with two output slots
 ]
 
 
-@pytest.mark.parametrize("mode", ["lean", "batch", "fallback"])
+LEAN_MIN_SEARCH = 1048576  # debug flag: k_lean ranks L0 by minimum searches also for L0 >= 8
+
+
+@pytest.mark.parametrize("mode", ["lean", "lean_min_search", "batch", "fallback"])
 @pytest.mark.parametrize("cfgi", range(len(CONFIGS)))
 def test_bound_accumulate_matches_oracle(ex, cfgi, mode):
     n, U, P, z, L0, Linf, vb, pb, mask = CONFIGS[cfgi]
@@ -85,7 +91,8 @@ def test_bound_accumulate_matches_oracle(ex, cfgi, mode):
     bp = o.BoundParams(L0, Linf, *(vb or (None, None)), *(pb or (None, None)))
     need_val = bool(mask & (2 | 4 | 8))
     _, _, rc, cnt, x, y = run_gpu(ex, pid, pk, val if need_val else None, U, P, bp, mask, seed=77 + cfgi,
-                                  fallback=mode == "fallback", debug_flags=BATCH_KERNEL if mode == "batch" else 0)
+                                  fallback=mode == "fallback",
+                                  debug_flags={"batch": BATCH_KERNEL, "lean_min_search": LEAN_MIN_SEARCH}.get(mode, 0))
     ref = o.bound_and_accumulate(pid, pk, val if need_val else None, P, bp, "hash", seed=77 + cfgi)
     check_acc(ref, rc, cnt, x, y, mask, val)
     if cfgi == 5 and mode != "fallback":
