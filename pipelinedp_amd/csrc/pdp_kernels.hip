@@ -106,18 +106,6 @@ __device__ __forceinline__ void st_rec(Rec* p, const Rec& r) {
 #endif
 }
 
-// Intermediate radix-pass layout ("split records"): pid / pk / value in
-// three arrays, so the per-tile digit upsweep of the next pass reads 4 B of
-// pid per row instead of the whole 16-B record.  K2 reads the AoS Rec
-// written by the last pass.
-struct SplitRecs {
-  uint32_t* pid;
-  uint32_t* pk;
-  double* val;
-};
-
-enum RecIO { kIoColumns = 0, kIoRec = 1, kIoSplit = 2 };
-
 struct KeySpec {
   int mode;  // 0: key = pid >> low ; 1: key = (pid << pkb) | pk ; 3: key = (pid, bits(val)) 96-bit
   int passes;
@@ -164,6 +152,7 @@ constexpr int kDebugLookback = 131072;  // radix passes by decoupled look-back i
 constexpr int kDebugNoAtomics = 262144;  // K2 skips its accumulator atomics (timing ablation)
 constexpr int kDebugNoHotCache = 524288;  // k_lean emits straight to HBM (no LDS partition cache)
 constexpr int kDebugLeanMinSearch = 1048576;  // k_lean ranks L0 by minimum searches even when L0 >= kSortMinL0
+constexpr int kDebugWalkOnly = 2097152;  // k_lean loads rows and finds segments only (timing floor, results invalid)
 
 struct AccPtrs {
   unsigned long long* row_count;
@@ -352,11 +341,12 @@ __global__ __launch_bounds__(kThreads) void k_histogram_tiles(const int64_t* __r
   if (invalid) atomicAdd(&counters[kCtrInvalid], (unsigned long long)invalid);
 }
 
-// K1u (upsweep of a records pass): digit count of every tile of the pass
-// input -- from the pid array alone when the input is split records (4 B per
-// row; key mode 0, i.e. the main path's pid sort), else from the records.
-template <bool SPLIT>
-__global__ __launch_bounds__(kThreads) void k_tile_counts(const Rec* __restrict__ rin, const uint32_t* __restrict__ pin,
+// K1u (upsweep of a records pass): digit count of every tile of `rin`.
+// (Tried: pid / pk / value split into three arrays between passes so this
+// reads 4 B per row -- it did, 2.1 -> 0.95 ms per launch at c3, but the
+// 4- and 8-byte digit-run scatters of the passes cost more: pass 0 11.3 ->
+// 17.4 ms.  Records stay 16-B AoS.)
+__global__ __launch_bounds__(kThreads) void k_tile_counts(const Rec* __restrict__ rin,
                                                           const unsigned long long* __restrict__ counters_n,
                                                           int n_slot, KeySpec ks, int pass, int64_t tiles,
                                                           unsigned int* __restrict__ tile_cnt) {
@@ -370,15 +360,7 @@ __global__ __launch_bounds__(kThreads) void k_tile_counts(const Rec* __restrict_
 #pragma unroll 4
     for (int k = 0; k < kItems; ++k) {
       const int64_t i = base + (int64_t)k * kThreads;
-      if (i < n) {
-        if (SPLIT) {
-          Rec r;
-          r.pid = pin[i];
-          atomicAdd(&st[digit_of(ks, pass, r)], 1u);
-        } else {
-          atomicAdd(&st[digit_of(ks, pass, rin[i])], 1u);
-        }
-      }
+      if (i < n) atomicAdd(&st[digit_of(ks, pass, rin[i])], 1u);
     }
     __syncthreads();
     tile_cnt[tile * 256 + t] = st[t];
@@ -470,10 +452,10 @@ constexpr int kLookback = PDP_LOOKBACK;
 constexpr int kHalfTile = kTile / PDP_OS_STAGE_DIV;
 constexpr uint32_t kNoPos = 0xFFFFu;
 
-template <int IN, int OUT>
+template <bool SOA>
 __global__ __launch_bounds__(kThreads, PDP_OS_OCC) void k_onesweep(
     const int64_t* __restrict__ pid, const int64_t* __restrict__ pk, const double* __restrict__ val,
-    const Rec* __restrict__ rin, Rec* __restrict__ rout, SplitRecs sin, SplitRecs sout, int64_t n_in,
+    const Rec* __restrict__ rin, Rec* __restrict__ rout, int64_t n_in,
     const unsigned long long* __restrict__ counters_n, int n_slot, KeySpec ks, int pass,
     const unsigned long long* __restrict__ off, unsigned long long* __restrict__ status, uint32_t epoch,
     unsigned long long* __restrict__ counters, int tile_slot, const unsigned int* __restrict__ tile_base) {
@@ -485,7 +467,6 @@ __global__ __launch_bounds__(kThreads, PDP_OS_OCC) void k_onesweep(
   __shared__ unsigned int s_tile;
   __shared__ unsigned int s_total;
 
-  constexpr bool SOA = IN == kIoColumns;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const long long c0 = ks.prof ? (long long)__builtin_amdgcn_s_memtime() : 0;
   // Reduce-then-scan mode (tile_base != null): tile = block, its digit bases
@@ -519,11 +500,6 @@ __global__ __launch_bounds__(kThreads, PDP_OS_OCC) void k_onesweep(
           d = 256;  // dropped
         else
           d = digit_of(ks, pass, r[k]);
-      } else if (IN == kIoSplit) {
-        r[k].pid = sin.pid[idx];
-        r[k].pk = sin.pk[idx];
-        r[k].val = sin.val[idx];
-        d = digit_of(ks, pass, r[k]);
       } else {
         r[k] = ld_rec(rin + idx);
         d = digit_of(ks, pass, r[k]);
@@ -702,15 +678,10 @@ __global__ __launch_bounds__(kThreads, PDP_OS_OCC) void k_onesweep(
     const unsigned int e = tot - h < (unsigned int)kHalfTile ? tot - h : (unsigned int)kHalfTile;
     for (unsigned int i = t; i < e; i += kThreads) {
       const Rec rc = s_rec[i];
-      const long long pos = (ks.ablate & kDebugLinearWrite) ? tile_start + (long long)(h + i)
-                                                            : s_gbase[digit_of(ks, pass, rc)] + (long long)(h + i);
-      if (OUT == kIoSplit) {
-        sout.pid[pos] = rc.pid;
-        sout.pk[pos] = rc.pk;
-        sout.val[pos] = rc.val;
-      } else {
-        st_rec(rout + pos, rc);
-      }
+      if (ks.ablate & kDebugLinearWrite)
+        st_rec(rout + tile_start + (long long)(h + i), rc);
+      else
+        st_rec(rout + s_gbase[digit_of(ks, pass, rc)] + (long long)(h + i), rc);
     }
     __syncthreads();
   }
@@ -1216,8 +1187,7 @@ struct Layout {
 Layout layout_for(int64_t n, bool sweep = false) {
   Layout L{};
   size_t o = 0;
-  // + 1 KiB: room for the 256-B aligned split-record arrays (pid / pk / value)
-  const size_t rb = align_up((size_t)std::max<int64_t>(n, 1) * sizeof(Rec) + 1024, 256);
+  const size_t rb = align_up((size_t)std::max<int64_t>(n, 1) * sizeof(Rec), 256);
   L.recs_a = o; o += rb;
   L.recs_b = o; o += rb;
   L.recs_c = o; o += sweep ? rb : 0;  // sweep: generic-path scratch that keeps the sorted rows intact
@@ -1458,18 +1428,18 @@ int sort_recs(pdp_ctx* ctx, Rec* a, Rec* b, int64_t m, const KeySpec& ks, unsign
     const unsigned int* bases = nullptr;
     if (rts) {
       const TileScan ts = tile_scan_bufs(ctx, status, tiles);
-      hipLaunchKernelGGL(k_tile_counts<false>, dim3(grid_for(tiles, 1, 4096)), dim3(kThreads), 0, stream, src,
-                         (const uint32_t*)nullptr, counters, (int)kCtrNGeneric, ks, p, tiles, ts.tile_cnt);
+      hipLaunchKernelGGL(k_tile_counts, dim3(grid_for(tiles, 1, 4096)), dim3(kThreads), 0, stream, src, counters,
+                         (int)kCtrNGeneric, ks, p, tiles, ts.tile_cnt);
       tile_scan(ts, off + p * kHist, stream);
       bases = ts.tile_cnt;
     } else {
       int rc = next_epoch(ctx, stream, status, status_bytes, ws);
       if (rc) return rc;
     }
-    hipLaunchKernelGGL((k_onesweep<kIoRec, kIoRec>), dim3((unsigned)tiles), dim3(kThreads), 0, stream,
-                       (const int64_t*)nullptr, (const int64_t*)nullptr, (const double*)nullptr, src, dst,
-                       SplitRecs{}, SplitRecs{}, m, counters, (int)kCtrNGeneric, ks, p, off + p * kHist, status,
-                       ctx->epoch, counters, (int)ctx->tile_slot++, bases);
+    hipLaunchKernelGGL(k_onesweep<false>, dim3((unsigned)tiles), dim3(kThreads), 0, stream,
+                       (const int64_t*)nullptr, (const int64_t*)nullptr, (const double*)nullptr, src, dst, m,
+                       counters, (int)kCtrNGeneric, ks, p, off + p * kHist, status, ctx->epoch, counters,
+                       (int)ctx->tile_slot++, bases);
     std::swap(src, dst);
   }
   HIP_TRY(hipGetLastError());
@@ -1891,21 +1861,13 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
                      (int)kCtrNKept);
   Rec* src = nullptr;
   Rec* dst = recs_a;
-  // pass p writes split records unless it is the last pass (K2 reads Rec)
-  auto split_of = [&](Rec* buf) {
-    char* b = (char*)buf;
-    const size_t q = align_up((size_t)n * 4, 256);
-    return SplitRecs{(uint32_t*)b, (uint32_t*)(b + q), (double*)(b + 2 * q)};
-  };
   for (int p = 0; p < ks.passes; ++p) {
     const unsigned int* bases = nullptr;
-    const bool last = p == ks.passes - 1;
     if (rts) {
       ProfScope ps(ctx, PDP_STAGE_TILE_COUNTS, stream);
       if (p > 0)
-        hipLaunchKernelGGL(k_tile_counts<true>, dim3(grid_for(L.tiles, 1, 4096)), dim3(kThreads), 0, stream,
-                           (const Rec*)nullptr, (const uint32_t*)split_of(src).pid, counters, (int)kCtrNKept, ks, p,
-                           L.tiles, ts.tile_cnt);
+        hipLaunchKernelGGL(k_tile_counts, dim3(grid_for(L.tiles, 1, 4096)), dim3(kThreads), 0, stream, src, counters,
+                           (int)kCtrNKept, ks, p, L.tiles, ts.tile_cnt);
       tile_scan(ts, off + p * kHist, stream);
       bases = ts.tile_cnt;
     } else {
@@ -1913,27 +1875,15 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
       if (rc) return rc;
     }
     ProfScope ps(ctx, p == 0 ? PDP_STAGE_ONESWEEP_FIRST : PDP_STAGE_ONESWEEP_REST, stream);
-    const SplitRecs sin = p > 0 ? split_of(src) : SplitRecs{};
-    const SplitRecs sout = last ? SplitRecs{} : split_of(dst);
-    const dim3 g((unsigned)L.tiles), b(kThreads);
-    const unsigned long long* offp = off + p * kHist;
-    const int slot = (int)ctx->tile_slot++;
-    if (p == 0 && last)
-      hipLaunchKernelGGL((k_onesweep<kIoColumns, kIoRec>), g, b, 0, stream, cols->pid, cols->pk, cols->value,
-                         (const Rec*)nullptr, dst, sin, sout, n, counters, (int)kCtrNKept, ks, p, offp, status,
-                         ctx->epoch, counters, slot, bases);
-    else if (p == 0)
-      hipLaunchKernelGGL((k_onesweep<kIoColumns, kIoSplit>), g, b, 0, stream, cols->pid, cols->pk, cols->value,
-                         (const Rec*)nullptr, dst, sin, sout, n, counters, (int)kCtrNKept, ks, p, offp, status,
-                         ctx->epoch, counters, slot, bases);
-    else if (last)
-      hipLaunchKernelGGL((k_onesweep<kIoSplit, kIoRec>), g, b, 0, stream, (const int64_t*)nullptr,
-                         (const int64_t*)nullptr, (const double*)nullptr, (const Rec*)nullptr, dst, sin, sout, n,
-                         counters, (int)kCtrNKept, ks, p, offp, status, ctx->epoch, counters, slot, bases);
+    if (p == 0)
+      hipLaunchKernelGGL(k_onesweep<true>, dim3((unsigned)L.tiles), dim3(kThreads), 0, stream, cols->pid, cols->pk,
+                         cols->value, (const Rec*)nullptr, dst, n, counters, (int)kCtrNKept, ks, p, off + p * kHist,
+                         status, ctx->epoch, counters, (int)ctx->tile_slot++, bases);
     else
-      hipLaunchKernelGGL((k_onesweep<kIoSplit, kIoSplit>), g, b, 0, stream, (const int64_t*)nullptr,
-                         (const int64_t*)nullptr, (const double*)nullptr, (const Rec*)nullptr, dst, sin, sout, n,
-                         counters, (int)kCtrNKept, ks, p, offp, status, ctx->epoch, counters, slot, bases);
+      hipLaunchKernelGGL(k_onesweep<false>, dim3((unsigned)L.tiles), dim3(kThreads), 0, stream,
+                         (const int64_t*)nullptr, (const int64_t*)nullptr, (const double*)nullptr, src, dst, n,
+                         counters, (int)kCtrNKept, ks, p, off + p * kHist, status, ctx->epoch, counters,
+                         (int)ctx->tile_slot++, bases);
     src = dst;
     dst = (dst == recs_a) ? recs_b : recs_a;
   }

@@ -74,13 +74,13 @@ CONFIGS = [
     (30000, 250, 20000, 0.0, 65, 3, (0.0, 10.0), None, 1 | 2),  # L0 > 64: lean with two output slots per lane
     (30000, 200, 20000, 0.0, 128, 2, (0.0, 10.0), None, 1 | 4 | 16),  # largest L0 of the lean kernel
     (30000, 200, 20000, 0.0, 129, 2, (0.0, 10.0), None, 1 | 2 | 16),  # L0 > 128: batch kernel
-    (40000, 400, 40, 1.1, 8, 2, (0.0, 10.0), None, 1 | 2 | 4 | 16),  # sorted K2 + second (L_inf) sort
-    (20000, 400, 12, 0.0, 9, 3, (-1.0, 4.0), None, 1 | 4 | 8),  # sorted K2, every group over L_inf
+    (40000, 400, 40, 1.1, 16, 2, (0.0, 10.0), None, 1 | 2 | 4 | 16),  # sorted K2 + second (L_inf) sort
+    (20000, 400, 12, 0.0, 17, 3, (-1.0, 4.0), None, 1 | 4 | 8),  # sorted K2, every group over L_inf
     (12000, 200, 500, 1.1, 70, 1, (0.0, 10.0), None, 1 | 2 | 16),  # sorted K2 with two output slots
 ]
 
 
-LEAN_MIN_SEARCH = 1048576  # debug flag: k_lean ranks L0 by minimum searches also for L0 >= 8
+LEAN_MIN_SEARCH = 1048576  # debug flag: k_lean ranks L0 by minimum searches also for L0 >= 16
 
 
 @pytest.mark.parametrize("mode", ["lean", "lean_min_search", "batch", "fallback"])

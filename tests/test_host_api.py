@@ -210,3 +210,29 @@ def test_columnar_partition_out_of_range_raises():
     acct.compute_budgets()
     with pytest.raises(ValueError, match="num_partitions"):
         list(res)
+
+
+def test_pipeline_dp_alias_runs_reference_caller_code():
+    # a reference caller (run_without_frameworks.py shape) with only the backend changed
+    import pipeline_dp
+    from cpu_executor import CpuExecutor
+    backend = pipeline_dp.HipBackend(sampling_seed=1, noise_seed=2)
+    backend._executor = CpuExecutor()
+    acct = pipeline_dp.NaiveBudgetAccountant(total_epsilon=100, total_delta=1e-6)
+    engine = pipeline_dp.DPEngine(acct, backend)
+    params = pipeline_dp.AggregateParams(noise_kind=pipeline_dp.NoiseKind.LAPLACE,
+                                         metrics=[pipeline_dp.Metrics.COUNT, pipeline_dp.Metrics.SUM],
+                                         max_partitions_contributed=3, max_contributions_per_partition=2,
+                                         min_value=1, max_value=5)
+    rows = [(u, f"movie{u % 4}", 1 + u % 5) for u in range(400)]
+    ext = pipeline_dp.DataExtractors(privacy_id_extractor=lambda r: r[0], partition_extractor=lambda r: r[1],
+                                     value_extractor=lambda r: r[2])
+    res = engine.aggregate(rows, params, ext)
+    acct.compute_budgets()
+    out = dict(res)
+    assert sorted(out) == [f"movie{i}" for i in range(4)]
+    assert all(abs(t.count - 100) < 10 for t in out.values())
+    import pipeline_dp.aggregate_params as ap
+    assert ap.AggregateParams is pipeline_dp.AggregateParams
+    with pytest.raises(AttributeError, match="HipBackend"):
+        pipeline_dp.LocalBackend  # noqa: B018
