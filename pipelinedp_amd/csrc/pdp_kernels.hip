@@ -1918,8 +1918,14 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
       const int64_t waves = (n + kLeanChunk - 1) / kLeanChunk;
       const int64_t blocks = (waves + 3) / 4 < kLeanMaxBlocks ? (waves + 3) / 4 : kLeanMaxBlocks;
       const bool sorted_l0 = bp->max_partitions_contributed >= kSortMinL0 && !(sp.debug & kDebugLeanMinSearch);
-      auto kern = bp->max_partitions_contributed <= 64 ? (sorted_l0 ? k_lean<1, true> : k_lean<1, false>)
-                                                       : (sorted_l0 ? k_lean<2, true> : k_lean<2, false>);
+      // the LDS partition cache pays when many privacy ids keep the same hot partitions, which grows with
+      // L0: c4 (L0 = 32) K2 137 -> 50 ms (round 1); at c3 (L0 = 4) / c2 (L0 = 8) it does not pay
+      const bool cache = bp->max_partitions_contributed >= kHotMinL0 && !(sp.debug & kDebugNoHotCache);
+      const bool two = bp->max_partitions_contributed > 64;
+      auto kern = sorted_l0 ? (two ? (cache ? k_lean<2, true, true> : k_lean<2, true, false>)
+                                   : (cache ? k_lean<1, true, true> : k_lean<1, true, false>))
+                            : (two ? (cache ? k_lean<2, false, true> : k_lean<2, false, false>)
+                                   : (cache ? k_lean<1, false, true> : k_lean<1, false, false>));
       hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), 0, stream, sorted, counters, (int)kCtrNKept, sp, acc,
                          ov, big, (int)bp->debug_force_fallback);
     } else {
