@@ -49,6 +49,21 @@ def analysis_oracle_cfgs(eps_sel=0.25, delta_sel=1e-6):
     return [ao.AnalysisConfig(l0, linf, lo, hi, "truncated_geometric", eps_sel, delta_sel) for l0, linf in SWEEP]
 
 
+def pmc_traffic(stage, rows):
+    """HBM bytes per launch of `stage` from profiles/pmc_traffic.json (written by
+    tools/pmc_traffic.py from the separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE
+    passes of tools/profile_round.sh) when that profile was taken on this same
+    workload size; (None, None) otherwise."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "pmc_traffic.json")) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None, None
+    if d.get("config_rows") != rows or stage not in d.get("bytes_per_launch", {}):
+        return None, None
+    return d["bytes_per_launch"][stage], d.get("round")
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -359,10 +374,15 @@ def main():
         nb = (P + world_size - 1) // world_size if world else P
         b = stage_bytes(dom, n, rows_after_public_filter, nb, len(fields))
         ach = b / (stages[dom]["ms_per_launch"] * 1e-3) / 1e9
+        traffic, prof_round = pmc_traffic(dom, n) if not sweep else (None, None)
         roofline = {"bound": "hbm", "kernel": dom, "achieved": round(ach, 1), "peak": PEAK_HBM_GBS,
                     "unit": "GB/s", "frac": round(ach / PEAK_HBM_GBS, 4), "traffic": None,
-                    "traffic_note": "HBM bytes need a separate rocprofv3 --pmc pass (FETCH_SIZE x2 on gfx950 + "
-                                    "WRITE_SIZE), committed under profiles/; not measurable inside this run",
+                    "traffic_note": "HBM bytes need separate rocprofv3 --pmc passes (FETCH_SIZE x2 on gfx950 + "
+                                    "WRITE_SIZE); not measurable inside this run",
+                    "traffic_carried": None if traffic is None else {
+                        "bytes_per_launch": traffic, "round": prof_round, "source": "profiles/pmc_traffic.json",
+                        "label": "CARRIED from the committed PMC profile of this workload size "
+                                 "(tools/profile_round.sh), not measured in this run"},
                     "algorithmic_bytes_per_launch": b,
                     "ms_per_launch_source": "hipEvents on the launch stream, averaged over the timed steps"}
         for s in stages:
