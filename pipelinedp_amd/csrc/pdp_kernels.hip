@@ -153,6 +153,8 @@ constexpr int kDebugNoAtomics = 262144;  // K2 skips its accumulator atomics (ti
 constexpr int kDebugNoHotCache = 524288;  // k_lean emits straight to HBM (no LDS partition cache)
 constexpr int kDebugLeanMinSearch = 1048576;  // k_lean ranks L0 by minimum searches even when L0 >= kSortMinL0
 constexpr int kDebugWalkOnly = 2097152;  // k_lean loads rows and finds segments only (timing floor, results invalid)
+constexpr int kDebugNoLinf = 8388608;     // k_lean skips the L_inf ranking (timing ablation, results invalid)
+constexpr int kDebugNoSums = 16777216;    // k_lean skips the kept-row sums (timing ablation, results invalid)
 
 struct AccPtrs {
   unsigned long long* row_count;
