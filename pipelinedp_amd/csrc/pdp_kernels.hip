@@ -2198,8 +2198,10 @@ int analysis_impl(pdp_ctx* ctx, const int64_t* pid, const int64_t* pk, const dou
   }
   if (priv) {
     const int64_t blocks = std::min<int64_t>((P + kAnaSelWaves - 1) / kAnaSelWaves, 16384);
-    hipLaunchKernelGGL(k_ana_select, dim3((unsigned)blocks, cgroups), dim3(64 * kAnaSelWaves), 0, stream, pref, npart,
-                       pbeg, P, cfg_d, nconf, (const double*)mom, out->prob_keep);
+    hipLaunchKernelGGL(k_ana_select<true>, dim3((unsigned)blocks, cgroups), dim3(64 * kAnaSelWaves), 0, stream, pref,
+                       npart, pbeg, P, cfg_d, nconf, (const double*)mom, out->prob_keep);
+    hipLaunchKernelGGL(k_ana_select<false>, dim3((unsigned)blocks, cgroups), dim3(64 * kAnaSelWaves), 0, stream, pref,
+                       npart, pbeg, P, cfg_d, nconf, (const double*)mom, out->prob_keep);
   }
   HIP_TRY(hipGetLastError());
   return 0;
