@@ -384,6 +384,9 @@ def main():
                         "label": "CARRIED from the committed PMC profile of this workload size "
                                  "(tools/profile_round.sh), not measured in this run"},
                     "algorithmic_bytes_per_launch": b,
+                    **({"bound_note": "c5 kernels are fp64-VALU bound (per-(pair, configuration) SumMetrics terms, "
+                                      "Poisson-binomial pmf per partition); the HBM fraction is reported for "
+                                      "completeness only"} if sweep else {}),
                     "ms_per_launch_source": "hipEvents on the launch stream, averaged over the timed steps"}
         for s in stages:
             bs = stage_bytes(s, n, rows_after_public_filter, nb, len(fields))

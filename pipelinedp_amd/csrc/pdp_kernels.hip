@@ -114,7 +114,7 @@ struct KeySpec {
   int low;
   int pkb;
   uint64_t seed;
-  uint32_t num_pids;
+  uint64_t num_pids;  // up to 2^32 (pid values 0 .. 2^32 - 1)
   uint32_t num_parts;
   int prof;  // accumulate per-phase s_memtime cycles of k_onesweep (kDebugSweepStamps)
   int ablate;  // kDebugNoLookback / kDebugLinearWrite (timing ablations, results invalid)
@@ -1449,7 +1449,7 @@ int sort_recs(pdp_ctx* ctx, Rec* a, Rec* b, int64_t m, const KeySpec& ks, unsign
   return 0;
 }
 
-KeySpec composite_spec(int mode, int hi_bits, int lo_bits, int pkb, uint32_t U, uint32_t P) {
+KeySpec composite_spec(int mode, int hi_bits, int lo_bits, int pkb, uint64_t U, uint32_t P) {
   KeySpec ks{};
   ks.mode = mode;
   ks.low = 0;
@@ -1480,7 +1480,7 @@ KeySpec composite_spec(int mode, int hi_bits, int lo_bits, int pkb, uint32_t U, 
 // (== sorted on the single-config path, a third buffer in a sweep so the
 // sorted rows survive for the next configuration).
 int run_generic(pdp_ctx* ctx, const Rec* sorted, Rec* spare, Rec* alt, const std::vector<unsigned long long>& ranges,
-                const Plan& plan, const SegParams& sp, const pdp_bound_params* bp, uint32_t U, uint32_t P,
+                const Plan& plan, const SegParams& sp, const pdp_bound_params* bp, uint64_t U, uint32_t P,
                 AccPtrs acc, unsigned long long* hist, unsigned long long* off, unsigned long long* counters,
                 unsigned long long* status, size_t status_bytes, void* ws, hipStream_t stream) {
   const int nr = (int)(ranges.size() / 2);
@@ -1834,7 +1834,7 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
   ks.low = plan.low;
   ks.pkb = plan.pkb;
   ks.seed = bp->sampling_seed;
-  ks.num_pids = (uint32_t)std::min<int64_t>(U, 0xFFFFFFFFll);
+  ks.num_pids = (uint64_t)U;
   ks.num_parts = (uint32_t)P;
   ks.passes = plan.passes;
   {

@@ -99,6 +99,25 @@ def test_bound_accumulate_matches_oracle(ex, cfgi, mode):
         assert ex.stats().fallback_rows > 0  # huge privacy ids went through the generic path
 
 
+def test_full_width_privacy_ids_and_wide_partition_ids(ex):
+    """Privacy ids over the whole 32-bit domain (U = 2^32, including 0 and
+    2^32 - 1: four radix passes) and partition ids near a 2^24 + 1 domain,
+    binding bounds, against the oracle."""
+    rng = np.random.default_rng(2024)
+    U, P, n = 1 << 32, (1 << 24) + 1, 40000
+    ids = np.unique(np.concatenate([[0, U - 1], rng.integers(0, U, 600)]))
+    pid = rng.choice(ids, n).astype(np.int64)
+    pid[:50] = U - 1
+    pk = rng.choice(np.concatenate([[0, P - 1], rng.integers(0, P, 900)]), n).astype(np.int64)
+    val = rng.uniform(-5, 15, n)
+    bp = o.BoundParams(3, 2, 0.0, 10.0)
+    for fallback in (False, True):
+        _, _, rc, cnt, x, _ = run_gpu(ex, pid, pk, val, U, P, bp, 1 | 4 | 16, seed=31, fallback=fallback)
+        ref = o.bound_and_accumulate(pid, pk, val, P, bp, "hash", seed=31)
+        check_acc(ref, rc, cnt, x, None, 1 | 4 | 16, val)
+    assert ex.stats().sort_passes == 4
+
+
 def test_dropped_rows_and_public_partitions(ex):
     n, U, P = 20000, 800, 400
     pid, pk, val = o.synth_rows(n, U, P, seed=9)
