@@ -155,6 +155,8 @@ constexpr int kDebugLeanMinSearch = 1048576;  // k_lean ranks L0 by minimum sear
 constexpr int kDebugWalkOnly = 2097152;  // k_lean loads rows and finds segments only (timing floor, results invalid)
 constexpr int kDebugNoLinf = 8388608;     // k_lean skips the L_inf ranking (timing ablation, results invalid)
 constexpr int kDebugNoSums = 16777216;    // k_lean skips the kept-row sums (timing ablation, results invalid)
+constexpr int kDebugForceHotCache = 33554432;  // k_lean uses the LDS partition cache at any L0
+constexpr int kDebugFewBlocks = 67108864;      // k_lean grid of 4096 blocks (longer grid-stride per block)
 
 struct AccPtrs {
   unsigned long long* row_count;
@@ -1918,11 +1920,13 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
     ProfScope ps(ctx, PDP_STAGE_BUCKETS, stream);
     if (bp->max_partitions_contributed <= kLeanMaxL0 && !(sp.debug & kDebugBatchKernel)) {
       const int64_t waves = (n + kLeanChunk - 1) / kLeanChunk;
-      const int64_t blocks = (waves + 3) / 4 < kLeanMaxBlocks ? (waves + 3) / 4 : kLeanMaxBlocks;
+      const int64_t max_blocks = (sp.debug & kDebugFewBlocks) ? 4096 : kLeanMaxBlocks;
+      const int64_t blocks = (waves + 3) / 4 < max_blocks ? (waves + 3) / 4 : max_blocks;
       const bool sorted_l0 = bp->max_partitions_contributed >= kSortMinL0 && !(sp.debug & kDebugLeanMinSearch);
       // the LDS partition cache pays when many privacy ids keep the same hot partitions, which grows with
       // L0: c4 (L0 = 32) K2 137 -> 50 ms (round 1); at c3 (L0 = 4) / c2 (L0 = 8) it does not pay
-      const bool cache = bp->max_partitions_contributed >= kHotMinL0 && !(sp.debug & kDebugNoHotCache);
+      const bool cache = (bp->max_partitions_contributed >= kHotMinL0 || (sp.debug & kDebugForceHotCache)) &&
+                         !(sp.debug & kDebugNoHotCache);
       const bool two = bp->max_partitions_contributed > 64;
       auto kern = sorted_l0 ? (two ? (cache ? k_lean<2, true, true> : k_lean<2, true, false>)
                                    : (cache ? k_lean<1, true, true> : k_lean<1, true, false>))
