@@ -293,6 +293,7 @@ typedef struct pdp_stats {
   int32_t bucket_low_bits;
   int64_t sweep_cycles[4];     /* radix passes, debug stamps only: load, rank, look-back/bases, scatter */
   int64_t sweep_tiles;
+  int64_t filter_rows;         /* rows that survived the L0 pre-filter (0: the filter did not run) */
 } pdp_stats;
 int pdp_get_stats(pdp_ctx* ctx, pdp_stats* out);
 
@@ -309,7 +310,9 @@ enum {
   PDP_STAGE_TILE_COUNTS = 7,     /* K1u per-tile digit counts (passes >= 1) + tile-offset scans */
   PDP_STAGE_ANALYSIS_PAIRS = 8,  /* utility analysis: (pk, pid) sort + per-pair pre-aggregation */
   PDP_STAGE_ANALYSIS_METRICS = 9, /* utility analysis: per-configuration partition metrics + selection */
-  PDP_NUM_STAGES = 10,
+  PDP_STAGE_FILTER = 10,        /* K1f L0 pre-filter (one workgroup per privacy-id bucket) */
+  PDP_STAGE_SURVIVOR_SORT = 11, /* radix sort of the pre-filter's survivors */
+  PDP_NUM_STAGES = 12,
 };
 int pdp_profile_enable(pdp_ctx* ctx, int enable);
 /* Waits for recorded events; adds into ms_out/launches_out[PDP_NUM_STAGES]

@@ -21,6 +21,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -63,6 +64,7 @@ enum Counter {
   kCtrSweepCycles = 8,  // 8..11: onesweep load / rank / look-back / scatter cycles (profiling)
   kCtrSweepTiles = 12,
   kCtrAnaPairs = 13,  // utility analysis: pairs of sampled partitions
+  kCtrNSurv = 14,     // rows that survive the L0 pre-filter (pdp_filter.inc)
   kCtrTile0 = 16,  // 16..63 tile claim counters, one per onesweep launch
 };
 
@@ -107,7 +109,8 @@ __device__ __forceinline__ void st_rec(Rec* p, const Rec& r) {
 }
 
 struct KeySpec {
-  int mode;  // 0: key = pid >> low ; 1: key = (pid << pkb) | pk ; 3: key = (pid, bits(val)) 96-bit
+  int mode;  // 0: key = pid >> low ; 1: key = (pid << pkb) | pk ; 3: key = (pid, bits(val)) 96-bit ;
+             // 4: bucketed pid: passes with shift >= 64 take the bucket digit (pid * mult) >> 32, others pid bits
   int passes;
   int shift[kMaxPasses];
   int bits[kMaxPasses];
@@ -116,6 +119,7 @@ struct KeySpec {
   uint64_t seed;
   uint64_t num_pids;  // up to 2^32 (pid values 0 .. 2^32 - 1)
   uint32_t num_parts;
+  uint64_t mult;  // mode 4: bucket digit multiplier (pdp_filter.inc)
   int prof;  // accumulate per-phase s_memtime cycles of k_onesweep (kDebugSweepStamps)
   int ablate;  // kDebugNoLookback / kDebugLinearWrite (timing ablations, results invalid)
 };
@@ -157,6 +161,9 @@ constexpr int kDebugNoLinf = 8388608;     // k_lean skips the L_inf ranking (tim
 constexpr int kDebugNoSums = 16777216;    // k_lean skips the kept-row sums (timing ablation, results invalid)
 constexpr int kDebugForceHotCache = 33554432;  // k_lean uses the LDS partition cache at any L0
 constexpr int kDebugFewBlocks = 67108864;      // k_lean grid of 4096 blocks (longer grid-stride per block)
+constexpr int kDebugNoFilter = 134217728;      // never use the L0 pre-filter (pdp_filter.inc)
+constexpr int kDebugForceFilter = 268435456;   // use the L0 pre-filter whenever it applies (small inputs too)
+constexpr int kDebugNoThin = 536870912;        // bound the pre-filter's survivors with k_lean instead of k_thin
 
 struct AccPtrs {
   unsigned long long* row_count;
@@ -178,6 +185,9 @@ __device__ __forceinline__ uint32_t digit_of(const KeySpec& ks, int pass, const 
   uint64_t key;
   if (ks.mode == 0) {
     key = (uint64_t)(r.pid >> ks.low);
+  } else if (ks.mode == 4) {
+    if (sh >= 64) return (uint32_t)(((uint64_t)r.pid * ks.mult) >> 32);
+    key = (uint64_t)r.pid;
   } else if (ks.mode == 1) {
     key = ((uint64_t)r.pid << ks.pkb) | (uint64_t)r.pk;
   } else {
@@ -436,6 +446,8 @@ __global__ __launch_bounds__(kThreads) void k_offsets(const unsigned long long* 
   if (threadIdx.x == 0) counters[n_slot] = (unsigned long long)n - hist[256];
 }
 
+#include "pdp_filter.inc"
+
 // ---------------------------------------------------------------------------
 // K1: one stable LSD radix pass, single sweep with decoupled look-back.
 // ---------------------------------------------------------------------------
@@ -456,14 +468,20 @@ constexpr int kLookback = PDP_LOOKBACK;
 constexpr int kHalfTile = kTile / PDP_OS_STAGE_DIV;
 constexpr uint32_t kNoPos = 0xFFFFu;
 
-template <bool SOA>
+// TAG (the bucket pass of the L0 pre-filter, pdp_filter.inc): also writes,
+// for every kept row, tag = (pid - first pid of its bucket) << 5 | level of
+// its group priority, into tag_out at the row's sorted position.
+template <bool SOA, bool TAG = false>
 __global__ __launch_bounds__(kThreads, PDP_OS_OCC) void k_onesweep(
     const int64_t* __restrict__ pid, const int64_t* __restrict__ pk, const double* __restrict__ val,
     const Rec* __restrict__ rin, Rec* __restrict__ rout, int64_t n_in,
     const unsigned long long* __restrict__ counters_n, int n_slot, KeySpec ks, int pass,
     const unsigned long long* __restrict__ off, unsigned long long* __restrict__ status, uint32_t epoch,
-    unsigned long long* __restrict__ counters, int tile_slot, const unsigned int* __restrict__ tile_base) {
+    unsigned long long* __restrict__ counters, int tile_slot, const unsigned int* __restrict__ tile_base,
+    uint32_t* __restrict__ tag_out, const uint32_t* __restrict__ tag_lo) {
   __shared__ Rec s_rec[kHalfTile];
+  __shared__ uint32_t s_tag[TAG ? kHalfTile : 1];
+  __shared__ uint32_t s_lo[TAG ? 256 : 1];
   __shared__ unsigned int s_cnt[4][kHist + 1];
   __shared__ unsigned int s_dstart[256];
   __shared__ long long s_gbase[256];
@@ -477,6 +495,7 @@ __global__ __launch_bounds__(kThreads, PDP_OS_OCC) void k_onesweep(
   // are precomputed; otherwise tiles are claimed in order for the look-back.
   if (t == 0 && !tile_base) s_tile = (unsigned int)atomicAdd(&counters[tile_slot], 1ull);
   for (int i = t; i < 4 * (kHist + 1); i += kThreads) (&s_cnt[0][0])[i] = 0;
+  if (TAG) s_lo[t] = tag_lo[t];
   __syncthreads();
   const int64_t tile = tile_base ? (int64_t)blockIdx.x : (int64_t)s_tile;
   // prefetch this tile's digit bases (their latency hides behind the loads)
@@ -489,6 +508,7 @@ __global__ __launch_bounds__(kThreads, PDP_OS_OCC) void k_onesweep(
 
   Rec r[kItems];
   uint32_t dr[kItems];  // digit (9 bits) | rank in wave << 9; later the sorted position
+  uint32_t tg[TAG ? kItems : 1];
   const int64_t base = tile_start + (int64_t)wave * (kItems * 64) + lane;
 #pragma unroll
   for (int k = 0; k < kItems; ++k) {
@@ -504,6 +524,9 @@ __global__ __launch_bounds__(kThreads, PDP_OS_OCC) void k_onesweep(
           d = 256;  // dropped
         else
           d = digit_of(ks, pass, r[k]);
+        if constexpr (TAG) {
+          if (d < 256) tg[k] = ((r[k].pid - s_lo[d]) << 5) | filt_level(filt_prio(ks.seed, r[k].pid, r[k].pk));
+        }
       } else {
         r[k] = ld_rec(rin + idx);
         d = digit_of(ks, pass, r[k]);
@@ -676,16 +699,22 @@ __global__ __launch_bounds__(kThreads, PDP_OS_OCC) void k_onesweep(
 #pragma unroll
     for (int k = 0; k < kItems; ++k) {
       const uint32_t q = dr[k] - h;
-      if (q < (uint32_t)kHalfTile) s_rec[q] = r[k];
+      if (q < (uint32_t)kHalfTile) {
+        s_rec[q] = r[k];
+        if constexpr (TAG) s_tag[q] = tg[k];
+      }
     }
     __syncthreads();
     const unsigned int e = tot - h < (unsigned int)kHalfTile ? tot - h : (unsigned int)kHalfTile;
     for (unsigned int i = t; i < e; i += kThreads) {
       const Rec rc = s_rec[i];
-      if (ks.ablate & kDebugLinearWrite)
+      if (ks.ablate & kDebugLinearWrite) {
         st_rec(rout + tile_start + (long long)(h + i), rc);
-      else
-        st_rec(rout + s_gbase[digit_of(ks, pass, rc)] + (long long)(h + i), rc);
+      } else {
+        const long long q = s_gbase[digit_of(ks, pass, rc)] + (long long)(h + i);
+        st_rec(rout + q, rc);
+        if constexpr (TAG) tag_out[q] = s_tag[i];
+      }
     }
     __syncthreads();
   }
@@ -746,6 +775,7 @@ __device__ __forceinline__ void emit_group(const SegParams& sp, const AccPtrs& a
 }
 
 #include "pdp_segments.inc"
+#include "pdp_thin.inc"
 #include "pdp_analysis.inc"
 
 // ---------------------------------------------------------------------------
@@ -1183,7 +1213,7 @@ int grid_for(int64_t n, int threads, int cap = 4096) {
 }
 
 struct Layout {
-  size_t recs_a, recs_b, recs_c, hist, off, counters, status, ranges, big, total;
+  size_t recs_a, recs_b, recs_c, hist, off, counters, status, ranges, big, tags, tag_lo, total;
   int64_t tiles;
   uint64_t big_cap;
 };
@@ -1203,6 +1233,8 @@ Layout layout_for(int64_t n, bool sweep = false) {
   L.ranges = o; o += align_up((size_t)kOverflowCap * 16, 256);
   L.big_cap = (uint64_t)std::max<int64_t>(n, 1) / 129 + 64;  // segments / batches of > 128 rows
   L.big = o; o += align_up((size_t)L.big_cap * 16, 256);
+  L.tags = o; o += sweep ? 0 : align_up((size_t)std::max<int64_t>(n, 1) * 4, 256);  // L0 pre-filter tags
+  L.tag_lo = o; o += 256 * 4;
   L.total = o;
   return L;
 }
@@ -1408,7 +1440,7 @@ void tile_scan(const TileScan& ts, const unsigned long long* off_pass, hipStream
 // sorted array pointer is returned in *out.
 int sort_recs(pdp_ctx* ctx, Rec* a, Rec* b, int64_t m, const KeySpec& ks, unsigned long long* hist,
               unsigned long long* off, unsigned long long* counters, unsigned long long* status, size_t status_bytes,
-              void* ws, hipStream_t stream, Rec** out) {
+              void* ws, hipStream_t stream, Rec** out, int stage = PDP_STAGE_GENERIC) {
   if (m <= 0 || ks.passes == 0) {
     *out = a;
     return 0;
@@ -1419,7 +1451,7 @@ int sort_recs(pdp_ctx* ctx, Rec* a, Rec* b, int64_t m, const KeySpec& ks, unsign
     ctx->tile_slot = kCtrTile0;
   }
   HIP_TRY(hipMemsetAsync(hist, 0, kMaxPasses * kHist * 8, stream));
-  ProfScope prof_generic(ctx, PDP_STAGE_GENERIC, stream);
+  ProfScope prof_generic(ctx, stage, stream);
   hipLaunchKernelGGL(k_histogram<false>, dim3(grid_for(m, kThreads, 2048)), dim3(kThreads), 0, stream,
                      (const int64_t*)nullptr, (const int64_t*)nullptr, a, m, ks, hist, counters);
   hipLaunchKernelGGL(k_offsets, dim3(1), dim3(kThreads), 0, stream, hist, off, ks.passes, m, counters,
@@ -1440,10 +1472,10 @@ int sort_recs(pdp_ctx* ctx, Rec* a, Rec* b, int64_t m, const KeySpec& ks, unsign
       int rc = next_epoch(ctx, stream, status, status_bytes, ws);
       if (rc) return rc;
     }
-    hipLaunchKernelGGL(k_onesweep<false>, dim3((unsigned)tiles), dim3(kThreads), 0, stream,
+    hipLaunchKernelGGL((k_onesweep<false, false>), dim3((unsigned)tiles), dim3(kThreads), 0, stream,
                        (const int64_t*)nullptr, (const int64_t*)nullptr, (const double*)nullptr, src, dst, m,
                        counters, (int)kCtrNGeneric, ks, p, off + p * kHist, status, ctx->epoch, counters,
-                       (int)ctx->tile_slot++, bases);
+                       (int)ctx->tile_slot++, bases, (uint32_t*)nullptr, (const uint32_t*)nullptr);
     std::swap(src, dst);
   }
   HIP_TRY(hipGetLastError());
@@ -1751,6 +1783,40 @@ int pdp_get_stats(pdp_ctx* ctx, pdp_stats* out) {
 
 namespace {
 
+// When the L0 pre-filter runs (pdp_filter.inc): small L0, enough rows per
+// privacy id for most of them to fall outside the kept partitions, and
+// buckets of at most kFiltWords privacy ids.
+struct FilterPlan {
+  bool on;
+  uint64_t mult;  // bucket digit = (pid * mult) >> 32
+  int low_bits;   // pid bits that tell the ids of one bucket apart
+};
+
+int env_int(const char* name, int def) {
+  const char* v = std::getenv(name);
+  return v && *v ? std::atoi(v) : def;
+}
+
+FilterPlan filter_plan(int64_t n, int64_t U, const pdp_bound_params* bp, int debug, bool sweep, bool rts) {
+  FilterPlan f{};
+  if (sweep || !rts || bp->bounds_already_enforced || (debug & kDebugNoFilter)) return f;
+  const int64_t l0 = bp->max_partitions_contributed;
+  if (l0 > kFiltMaxL0 || U < 1 || U > (1ll << 32)) return f;
+  if (!(debug & kDebugForceFilter) && (n < (1ll << 22) || n < 4 * l0 * U)) return f;
+  const uint64_t mult = (1ull << 40) / (uint64_t)U;  // floor: every digit <= 255
+  uint64_t width = 0;
+  for (uint64_t b = 0; b < 256; ++b) {
+    const uint64_t lo = filt_bucket_lo(b, mult);
+    const uint64_t hi = std::min<uint64_t>(filt_bucket_lo(b + 1, mult), (uint64_t)U);
+    if (hi > lo) width = std::max(width, hi - lo);
+  }
+  if (width > (uint64_t)kFiltWords) return f;
+  f.on = true;
+  f.mult = mult;
+  f.low_bits = std::max(1, pdp::ceil_log2_u64(width));
+  return f;
+}
+
 // pdp_bound_accumulate (nconf == 1, sweep == false) and
 // pdp_bound_accumulate_sweep: K0/K1 sort the rows by privacy id ONCE (the
 // order does not depend on L0 / L_inf / clipping), then K2 (+ KF) runs per
@@ -1847,11 +1913,23 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
       sh += plan.bits[i];
     }
   }
-  ctx->stats.sort_passes = plan.passes;
   ks.prof = (sp.debug & kDebugSweepStamps) != 0;
   ks.ablate = (sp.debug & kDebugSortOnly) ? (sp.debug & (kDebugNoLookback | kDebugLinearWrite)) : 0;
   const bool rts = use_tile_scan(n, sp.debug);
   const TileScan ts = rts ? tile_scan_bufs(ctx, status, L.tiles) : TileScan{};
+  // L0 pre-filter (pdp_filter.inc): one pass on the bucket digit instead of the full pid sort
+  const FilterPlan fpl = filter_plan(n, U, bp, sp.debug, sweep, rts);
+  uint32_t* tags = (uint32_t*)(ws + L.tags);
+  uint32_t* tag_lo = (uint32_t*)(ws + L.tag_lo);
+  if (fpl.on) {
+    ks.mode = 4;
+    ks.mult = fpl.mult;
+    ks.passes = 1;
+    ks.shift[0] = 64;
+    ks.bits[0] = 8;
+    hipLaunchKernelGGL(k_bucket_lo, dim3(1), dim3(256), 0, stream, fpl.mult, tag_lo);
+  }
+  ctx->stats.sort_passes = ks.passes;
   {
     ProfScope ps(ctx, PDP_STAGE_HISTOGRAM, stream);
     if (rts)
@@ -1879,15 +1957,20 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
       if (rc) return rc;
     }
     ProfScope ps(ctx, p == 0 ? PDP_STAGE_ONESWEEP_FIRST : PDP_STAGE_ONESWEEP_REST, stream);
-    if (p == 0)
-      hipLaunchKernelGGL(k_onesweep<true>, dim3((unsigned)L.tiles), dim3(kThreads), 0, stream, cols->pid, cols->pk,
-                         cols->value, (const Rec*)nullptr, dst, n, counters, (int)kCtrNKept, ks, p, off + p * kHist,
-                         status, ctx->epoch, counters, (int)ctx->tile_slot++, bases);
+    if (p == 0 && fpl.on)
+      hipLaunchKernelGGL((k_onesweep<true, true>), dim3((unsigned)L.tiles), dim3(kThreads), 0, stream, cols->pid,
+                         cols->pk, cols->value, (const Rec*)nullptr, dst, n, counters, (int)kCtrNKept, ks, p,
+                         off + p * kHist, status, ctx->epoch, counters, (int)ctx->tile_slot++, bases, tags, tag_lo);
+    else if (p == 0)
+      hipLaunchKernelGGL((k_onesweep<true, false>), dim3((unsigned)L.tiles), dim3(kThreads), 0, stream, cols->pid,
+                         cols->pk, cols->value, (const Rec*)nullptr, dst, n, counters, (int)kCtrNKept, ks, p,
+                         off + p * kHist, status, ctx->epoch, counters, (int)ctx->tile_slot++, bases,
+                         (uint32_t*)nullptr, (const uint32_t*)nullptr);
     else
-      hipLaunchKernelGGL(k_onesweep<false>, dim3((unsigned)L.tiles), dim3(kThreads), 0, stream,
+      hipLaunchKernelGGL((k_onesweep<false, false>), dim3((unsigned)L.tiles), dim3(kThreads), 0, stream,
                          (const int64_t*)nullptr, (const int64_t*)nullptr, (const double*)nullptr, src, dst, n,
                          counters, (int)kCtrNKept, ks, p, off + p * kHist, status, ctx->epoch, counters,
-                         (int)ctx->tile_slot++, bases);
+                         (int)ctx->tile_slot++, bases, (uint32_t*)nullptr, (const uint32_t*)nullptr);
     src = dst;
     dst = (dst == recs_a) ? recs_b : recs_a;
   }
@@ -1897,6 +1980,45 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
   if (sp.debug & kDebugSortOnly) {
     HIP_TRY(hipStreamSynchronize(stream));
     return 0;
+  }
+  int n_slot = kCtrNKept;  // counter holding the number of rows in `sorted`
+  uint64_t n_sorted = (uint64_t)n;  // upper bound of that number (grid sizes)
+  if (fpl.on) {
+    // K1f: survivors of the bucket-sorted rows -> spare (input order per pid kept)
+    HIP_TRY(hipMemsetAsync(counters + kCtrNSurv, 0, 8, stream));
+    {
+      ProfScope ps(ctx, PDP_STAGE_FILTER, stream);
+      hipLaunchKernelGGL(k_filter, dim3(256), dim3(kFiltThreads), 0, stream, sorted, tags, spare, off, counters,
+                         (int)kCtrNKept, (int)kCtrNSurv, (int)bp->max_partitions_contributed);
+    }
+    HIP_TRY(hipGetLastError());
+    unsigned long long m = 0;
+    HIP_TRY(hipMemcpyAsync(&m, counters + kCtrNSurv, 8, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipStreamSynchronize(stream));
+    ctx->stats.filter_rows = (int64_t)m;
+    // survivors by (bucket, pid & (2^low_bits - 1)): groups every pid (a bucket spans <= 2^low_bits ids)
+    KeySpec k2 = ks;
+    k2.passes = 0;
+    for (int sh = 0; sh < fpl.low_bits; sh += 8) {
+      k2.shift[k2.passes] = sh;
+      k2.bits[k2.passes] = std::min(8, fpl.low_bits - sh);
+      ++k2.passes;
+    }
+    k2.shift[k2.passes] = 64;
+    k2.bits[k2.passes] = 8;
+    ++k2.passes;
+    ctx->stats.sort_passes += k2.passes;
+    if (m == 0) HIP_TRY(hipMemsetAsync(counters + kCtrNGeneric, 0, 8, stream));
+    Rec* sa = spare;
+    Rec* sb = sorted;
+    Rec* out = nullptr;
+    int rc = sort_recs(ctx, sa, sb, (int64_t)m, k2, hist, off, counters, status, status_bytes, workspace, stream, &out,
+                       PDP_STAGE_SURVIVOR_SORT);
+    if (rc) return rc;
+    sorted = out;
+    spare = (out == sa) ? sb : sa;
+    n_slot = kCtrNGeneric;
+    n_sorted = m;
   }
 
   OvList ov{ranges, counters};
@@ -1918,35 +2040,45 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
   }
   {
     ProfScope ps(ctx, PDP_STAGE_BUCKETS, stream);
-    if (bp->max_partitions_contributed <= kLeanMaxL0 && !(sp.debug & kDebugBatchKernel)) {
-      const int64_t waves = (n + kLeanChunk - 1) / kLeanChunk;
-      const int64_t max_blocks = (sp.debug & kDebugFewBlocks) ? 4096 : kLeanMaxBlocks;
-      const int64_t blocks = (waves + 3) / 4 < max_blocks ? (waves + 3) / 4 : max_blocks;
+    const bool thin = fpl.on && bp->max_partitions_contributed <= kThinMaxL0 &&
+                      bp->max_contributions_per_partition <= kThinMaxLinf &&
+                      !(sp.debug & (kDebugBatchKernel | kDebugNoThin));
+    if (thin) {
+      const int64_t waves = ((int64_t)n_sorted + kThinChunk - 1) / kThinChunk;
+      const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((waves + 3) / 4, 8192));
+      hipLaunchKernelGGL(k_thin, dim3((unsigned)blocks), dim3(256), 0, stream, sorted, counters, n_slot, sp, acc, ov,
+                         (int)bp->debug_force_fallback);
+    } else if (bp->max_partitions_contributed <= kLeanMaxL0 && !(sp.debug & kDebugBatchKernel)) {
+      const int64_t waves = ((int64_t)n_sorted + kLeanChunk - 1) / kLeanChunk;
+      int64_t max_blocks = (sp.debug & kDebugFewBlocks) ? 4096 : kLeanMaxBlocks;
+      if (fpl.on) max_blocks = env_int("PDP_K2_BLOCKS", (int)max_blocks);
+      const int64_t blocks = std::max<int64_t>(1, (waves + 3) / 4 < max_blocks ? (waves + 3) / 4 : max_blocks);
       const bool sorted_l0 = bp->max_partitions_contributed >= kSortMinL0 && !(sp.debug & kDebugLeanMinSearch);
       // the LDS partition cache pays when many privacy ids keep the same hot partitions, which grows with
       // L0: c4 (L0 = 32) K2 137 -> 50 ms (round 1); at c3 (L0 = 4) / c2 (L0 = 8) it does not pay
-      const bool cache = (bp->max_partitions_contributed >= kHotMinL0 || (sp.debug & kDebugForceHotCache)) &&
+      const bool cache = (bp->max_partitions_contributed >= kHotMinL0 || (sp.debug & kDebugForceHotCache) ||
+                          (fpl.on && env_int("PDP_K2_CACHE", 0))) &&
                          !(sp.debug & kDebugNoHotCache);
       const bool two = bp->max_partitions_contributed > 64;
       auto kern = sorted_l0 ? (two ? (cache ? k_lean<2, true, true> : k_lean<2, true, false>)
                                    : (cache ? k_lean<1, true, true> : k_lean<1, true, false>))
                             : (two ? (cache ? k_lean<2, false, true> : k_lean<2, false, false>)
                                    : (cache ? k_lean<1, false, true> : k_lean<1, false, false>));
-      hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), 0, stream, sorted, counters, (int)kCtrNKept, sp, acc,
+      hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), 0, stream, sorted, counters, n_slot, sp, acc,
                          ov, big, (int)bp->debug_force_fallback);
     } else {
-      hipLaunchKernelGGL(k_segments, dim3((unsigned)seg_grid), dim3(kThreads), 0, stream, sorted, counters,
-                         (int)kCtrNKept, sp, acc, ov, big, (int)bp->debug_force_fallback);
+      hipLaunchKernelGGL(k_segments, dim3((unsigned)seg_grid), dim3(kThreads), 0, stream, sorted, counters, n_slot,
+                         sp, acc, ov, big, (int)bp->debug_force_fallback);
     }
     hipLaunchKernelGGL(k_segments_big, dim3(1024), dim3(64 * kBigWaves), 0, stream, sorted, counters, sp, acc, big);
   }
   HIP_TRY(hipGetLastError());
 
-  unsigned long long host_ctr[13];
+  unsigned long long host_ctr[kCtrNSurv + 1];
   HIP_TRY(hipMemcpyAsync(host_ctr, counters, sizeof(host_ctr), hipMemcpyDeviceToHost, stream));
   HIP_TRY(hipStreamSynchronize(stream));
   ctx->stats.kept_rows_in = (int64_t)host_ctr[kCtrNKept];
-  n_kept = host_ctr[kCtrNKept];
+  n_kept = host_ctr[n_slot];
   for (int i = 0; i < 4; ++i) ctx->stats.sweep_cycles[i] = (int64_t)host_ctr[kCtrSweepCycles + i];
   ctx->stats.sweep_tiles = (int64_t)host_ctr[kCtrSweepTiles];
   if (host_ctr[kCtrErr]) return fail(PDP_ERR_INTERNAL, "radix look-back timed out");
@@ -1958,7 +2090,7 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
     if (acc.count) HIP_TRY(hipMemsetAsync(acc.count, 0, (size_t)P * 8, stream));
     if (acc.x) HIP_TRY(hipMemsetAsync(acc.x, 0, (size_t)P * 8, stream));
     if (acc.y) HIP_TRY(hipMemsetAsync(acc.y, 0, (size_t)P * 8, stream));
-    rg = {0ull, host_ctr[kCtrNKept]};
+    rg = {0ull, host_ctr[n_slot]};
   } else if (host_ctr[kCtrNRanges]) {
     rg.resize(2 * host_ctr[kCtrNRanges]);
     HIP_TRY(hipMemcpyAsync(rg.data(), ranges, rg.size() * 8, hipMemcpyDeviceToHost, stream));

@@ -67,7 +67,7 @@ class AnalysisOutputs(ctypes.Structure):
 class Stats(ctypes.Structure):
     _fields_ = [("kept_rows_in", c_i64), ("fallback_rows", c_i64), ("fallback_ranges", c_i64),
                 ("sort_passes", c_i32), ("bucket_low_bits", c_i32), ("sweep_cycles", c_i64 * 4),
-                ("sweep_tiles", c_i64)]
+                ("sweep_tiles", c_i64), ("filter_rows", c_i64)]
 
 
 # Every symbol declared in include/pdp_hip.h: (name, restype, argtypes).
@@ -111,7 +111,7 @@ SIGNATURES = [
 ]
 
 STAGES = ["histogram", "onesweep_first", "onesweep_rest", "buckets", "generic", "release", "enforced",
-          "tile_counts", "analysis_pairs", "analysis_metrics"]
+          "tile_counts", "analysis_pairs", "analysis_metrics", "filter", "survivor_sort"]
 
 _lib = None
 

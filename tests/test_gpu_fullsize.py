@@ -15,13 +15,15 @@ plain torch ops on the same device-resident inputs:
   sum(privacy-id count) == sum_pid min(npk, L0) bit-exact; per pk
   row_count <= count <= min(Linf * row_count, rows of pk)
   (`contribution_bounders.py:74-76`); |sum(clip - mid)| <= count * (b - a) / 2;
-* determinism: a second run with the same seed gives identical counts.
+* the L0 pre-filter (on by default at this shape): a second run with the
+  filter disabled gives identical counts and privacy-id counts, sums to 1e-9.
 """
 import pytest
 
 pytestmark = pytest.mark.gpu
 
 MASK_COUNT, MASK_SUM, MASK_MEAN, MASK_PID = 1, 2, 4, 16
+NO_FILTER = 134217728  # debug flag: full pid sort, no L0 pre-filter
 
 
 @pytest.fixture(scope="module")
@@ -66,6 +68,7 @@ def test_headline_1b_rows_binding_invariants(ex):
     cfg = BoundConfig(mask, L0, Linf, a, b, sampling_seed=13)
     acc = ex.accumulate(pid, pk, val, U, P, cfg)
     torch.cuda.synchronize()
+    assert 0 < ex.stats().filter_rows < n // 5  # the pre-filter ran: survivors only go through the pid sort
     rc, cnt, nsum = acc.row_count.clone(), acc.count.clone(), acc.x.clone()
 
     rows_pk = torch.bincount(pk, minlength=P)
@@ -80,8 +83,10 @@ def test_headline_1b_rows_binding_invariants(ex):
     assert bool((nsum.abs() <= cnt.to(torch.float64) * (b - a) / 2 + 1e-6).all())
 
     pid, pk, val = ex.generate(n, U, P, seed=20250204, zipf_s=1.1, lo=a, hi=b)
-    acc2 = ex.accumulate(pid, pk, val, U, P, cfg)
+    nofilter = BoundConfig(mask, L0, Linf, a, b, sampling_seed=13, debug_flags=NO_FILTER)
+    acc2 = ex.accumulate(pid, pk, val, U, P, nofilter)
     torch.cuda.synchronize()
+    assert ex.stats().filter_rows == 0
     assert torch.equal(acc2.row_count, rc)
     assert torch.equal(acc2.count, cnt)
     absmax = cnt.to(torch.float64) * (b - a) / 2

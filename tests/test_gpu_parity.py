@@ -81,9 +81,14 @@ CONFIGS = [
 
 
 LEAN_MIN_SEARCH = 1048576  # debug flag: k_lean ranks L0 by minimum searches also for L0 >= 16
+NO_FILTER = 134217728  # debug flag: never use the L0 pre-filter
+FORCE_FILTER = 268435456  # debug flag: L0 pre-filter whenever L0 <= 8 (small inputs too)
+NO_THIN = 536870912  # debug flag: the pre-filter's survivors go through k_lean, not k_thin
+FILTER_MAX_L0 = 8
 
 
-@pytest.mark.parametrize("mode", ["lean", "lean_min_search", "batch", "fallback"])
+@pytest.mark.parametrize("mode", ["lean", "lean_min_search", "batch", "fallback", "filter", "filter_lean",
+                                  "filter_batch", "filter_fallback"])
 @pytest.mark.parametrize("cfgi", range(len(CONFIGS)))
 def test_bound_accumulate_matches_oracle(ex, cfgi, mode):
     n, U, P, z, L0, Linf, vb, pb, mask = CONFIGS[cfgi]
@@ -91,12 +96,42 @@ def test_bound_accumulate_matches_oracle(ex, cfgi, mode):
     bp = o.BoundParams(L0, Linf, *(vb or (None, None)), *(pb or (None, None)))
     need_val = bool(mask & (2 | 4 | 8))
     _, _, rc, cnt, x, y = run_gpu(ex, pid, pk, val if need_val else None, U, P, bp, mask, seed=77 + cfgi,
-                                  fallback=mode == "fallback",
-                                  debug_flags={"batch": BATCH_KERNEL, "lean_min_search": LEAN_MIN_SEARCH}.get(mode, 0))
+                                  fallback=mode in ("fallback", "filter_fallback"),
+                                  debug_flags={"batch": BATCH_KERNEL, "lean_min_search": LEAN_MIN_SEARCH,
+                                               "filter": FORCE_FILTER, "filter_fallback": FORCE_FILTER,
+                                               "filter_lean": FORCE_FILTER | NO_THIN,
+                                               "filter_batch": FORCE_FILTER | BATCH_KERNEL}.get(mode, 0))
     ref = o.bound_and_accumulate(pid, pk, val if need_val else None, P, bp, "hash", seed=77 + cfgi)
     check_acc(ref, rc, cnt, x, y, mask, val)
-    if cfgi == 5 and mode != "fallback":
-        assert ex.stats().fallback_rows > 0  # huge privacy ids went through the generic path
+    st = ex.stats()
+    if cfgi == 5 and "fallback" not in mode:
+        assert st.fallback_rows > 0  # huge privacy ids went through the generic path
+    if mode.startswith("filter"):
+        assert (st.filter_rows > 0) == (L0 <= FILTER_MAX_L0)  # the pre-filter ran (and kept rows)
+        if L0 <= FILTER_MAX_L0:
+            assert st.filter_rows <= n
+
+
+@pytest.mark.parametrize("L0,Linf,z", [(1, 1, 1.1), (2, 3, 0.0), (4, 2, 1.1), (8, 4, 0.0), (8, 1, 1.3)])
+def test_prefilter_matches_unfiltered_at_scale(ex, L0, Linf, z):
+    """The L0 pre-filter (automatic at this size: 2^22 rows, 100 rows per
+    privacy id) against the same run with the filter disabled, and both
+    against the oracle: counts and privacy-id counts bit-exact, sums to
+    1e-9; the survivors are a small share of the rows."""
+    n, U, P = 1 << 22, (1 << 22) // 100, 200000
+    pid, pk, val = o.synth_rows(n, U, P, seed=500 + L0, zipf_s=z, value_lo=-5, value_hi=15)
+    bp = o.BoundParams(L0, Linf, 0.0, 10.0)
+    mask = 1 | 2 | 4 | 16
+    _, _, rc, cnt, x, _ = run_gpu(ex, pid, pk, val, U, P, bp, mask, seed=9)
+    surv = ex.stats().filter_rows
+    assert 0 < surv < n // 2
+    _, _, rc2, cnt2, x2, _ = run_gpu(ex, pid, pk, val, U, P, bp, mask, seed=9, debug_flags=NO_FILTER)
+    assert ex.stats().filter_rows == 0
+    np.testing.assert_array_equal(rc, rc2)
+    np.testing.assert_array_equal(cnt, cnt2)
+    np.testing.assert_allclose(x, x2, rtol=1e-9, atol=1e-9)
+    ref = o.bound_and_accumulate(pid, pk, val, P, bp, "hash", seed=9)
+    check_acc(ref, rc, cnt, x, None, mask, val)
 
 
 def test_full_width_privacy_ids_and_wide_partition_ids(ex):
