@@ -2045,8 +2045,16 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
                       !(sp.debug & (kDebugBatchKernel | kDebugNoThin));
     if (thin) {
       const int64_t waves = ((int64_t)n_sorted + kThinChunk - 1) / kThinChunk;
-      const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((waves + 3) / 4, 8192));
-      hipLaunchKernelGGL(k_thin, dim3((unsigned)blocks), dim3(256), 0, stream, sorted, counters, n_slot, sp, acc, ov,
+      // LDS partition cache on: the Zipf-head pairs' HBM atomics otherwise dominate (c3: K2 8.1 -> 3.4 ms)
+      const bool tcache = env_int("PDP_THIN_CACHE", 1) != 0;
+      const int64_t blocks =
+          std::max<int64_t>(1, std::min<int64_t>((waves + 3) / 4, env_int("PDP_THIN_BLOCKS", 8192)));
+      const int64_t l0 = bp->max_partitions_contributed;
+      auto kern = l0 <= 1 ? (tcache ? k_thin<true, 1> : k_thin<false, 1>)
+                : l0 <= 2 ? (tcache ? k_thin<true, 2> : k_thin<false, 2>)
+                : l0 <= 4 ? (tcache ? k_thin<true, 4> : k_thin<false, 4>)
+                          : (tcache ? k_thin<true, 8> : k_thin<false, 8>);
+      hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), 0, stream, sorted, counters, n_slot, sp, acc, ov, big,
                          (int)bp->debug_force_fallback);
     } else if (bp->max_partitions_contributed <= kLeanMaxL0 && !(sp.debug & kDebugBatchKernel)) {
       const int64_t waves = ((int64_t)n_sorted + kLeanChunk - 1) / kLeanChunk;
