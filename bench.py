@@ -89,13 +89,20 @@ def parse():
     return args
 
 
-def stage_bytes(stage, n_in, n_kept, P, nfields):
-    """Algorithmic bytes of one launch of each kernel (Roofline)."""
+def stage_bytes(stage, n_in, n_kept, P, nfields, survivors=0, survivor_passes=0):
+    """Algorithmic bytes of one launch of each kernel (Roofline).
+    With the L0 pre-filter (survivors > 0): the first pass is the bucket pass
+    (+ a 4-B tag per row), k_filter reads the tags twice and moves the
+    survivors' records, and the survivor sort and K2 see the survivors only."""
+    sorted_rows = survivors if survivors else n_kept
     return {
         "histogram": 16 * n_in,  # read int64 pid + int64 pk
-        "onesweep_first": (24 + 16) * n_in,  # read 3 columns, write 16-B records
+        "onesweep_first": (24 + 16 + (4 if survivors else 0)) * n_in,  # read 3 columns, write 16-B records (+ tags)
         "onesweep_rest": 32 * n_kept,  # read + write 16-B records
-        "buckets": 16 * n_kept,  # read 16-B records once
+        "filter": 8 * n_kept + 32 * survivors,  # tags twice, survivors' records read + written
+        # histogram read + per pass (read + write) + per later pass an upsweep read
+        "survivor_sort": survivors * (16 + 32 * survivor_passes + 16 * max(survivor_passes - 1, 0)),
+        "buckets": 16 * sorted_rows,  # read 16-B records once
         "release": P * (3 * 8 + 1 + 8 * nfields),
         # c5: read the input columns once; read the (pk, privacy id, count, sum) pairs once and write
         # C x P x (3 metrics x 5 + keep probability) doubles
@@ -343,6 +350,8 @@ def main():
     torch.cuda.synchronize()
     st = ex.stats()
     rows_after_public_filter = int(st.kept_rows_in)
+    surv = int(st.filter_rows)  # rows that survive the L0 pre-filter (0: it did not run)
+    surv_passes = int(st.sort_passes) - 1 if surv else 0
     if not args.no_profile:
         ex.profile(True)
         ex.profile_read(reset=True)
@@ -372,7 +381,7 @@ def main():
                 stages[s] = {"ms_per_launch": ms / cnt, "launches_per_step": cnt / args.steps}
         dom = max(stages, key=lambda s: stages[s]["ms_per_launch"] * stages[s]["launches_per_step"])
         nb = (P + world_size - 1) // world_size if world else P
-        b = stage_bytes(dom, n, rows_after_public_filter, nb, len(fields))
+        b = stage_bytes(dom, n, rows_after_public_filter, nb, len(fields), surv, surv_passes)
         ach = b / (stages[dom]["ms_per_launch"] * 1e-3) / 1e9
         traffic, prof_round = pmc_traffic(dom, n) if not sweep else (None, None)
         roofline = {"bound": "hbm", "kernel": dom, "achieved": round(ach, 1), "peak": PEAK_HBM_GBS,
@@ -389,7 +398,7 @@ def main():
                                       "completeness only"} if sweep else {}),
                     "ms_per_launch_source": "hipEvents on the launch stream, averaged over the timed steps"}
         for s in stages:
-            bs = stage_bytes(s, n, rows_after_public_filter, nb, len(fields))
+            bs = stage_bytes(s, n, rows_after_public_filter, nb, len(fields), surv, surv_passes)
             if bs:
                 stages[s]["achieved_GBs"] = round(bs / (stages[s]["ms_per_launch"] * 1e-3) / 1e9, 1)
 
@@ -440,7 +449,8 @@ def main():
                                                 "L0=2, Linf=1"},
             "fp64_sums": "per-partition fp64 sums use fp64 atomics: summation order, hence the last bits, vary run "
                          "to run; counts and keep decisions are exact and deterministic",
-            "kernels": stages, "rows_after_public_filter": rows_after_public_filter, **kept,
+            "kernels": stages, "rows_after_public_filter": rows_after_public_filter,
+            "l0_prefilter_survivors": surv, **kept,
             "kept_partitions_rank0": kept_parts,
             "sort_passes": int(st.sort_passes), "bucket_low_bits": int(st.bucket_low_bits),
             "fallback_rows": int(st.fallback_rows),

@@ -164,6 +164,7 @@ constexpr int kDebugFewBlocks = 67108864;      // k_lean grid of 4096 blocks (lo
 constexpr int kDebugNoFilter = 134217728;      // never use the L0 pre-filter (pdp_filter.inc)
 constexpr int kDebugForceFilter = 268435456;   // use the L0 pre-filter whenever it applies (small inputs too)
 constexpr int kDebugNoThin = 536870912;        // bound the pre-filter's survivors with k_lean instead of k_thin
+constexpr int kDebugFilterTiming = 1073741824;  // k_filter timing ablation: phase 1 only (results invalid)
 
 struct AccPtrs {
   unsigned long long* row_count;
@@ -1989,7 +1990,8 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
     {
       ProfScope ps(ctx, PDP_STAGE_FILTER, stream);
       hipLaunchKernelGGL(k_filter, dim3(256), dim3(kFiltThreads), 0, stream, sorted, tags, spare, off, counters,
-                         (int)kCtrNKept, (int)kCtrNSurv, (int)bp->max_partitions_contributed);
+                         (int)kCtrNKept, (int)kCtrNSurv, (int)bp->max_partitions_contributed,
+                         (sp.debug & kDebugFilterTiming) != 0);
     }
     HIP_TRY(hipGetLastError());
     unsigned long long m = 0;
