@@ -65,6 +65,7 @@ enum Counter {
   kCtrSweepTiles = 12,
   kCtrAnaPairs = 13,  // utility analysis: pairs of sampled partitions
   kCtrNSurv = 14,     // rows that survive the L0 pre-filter (pdp_filter.inc)
+  kCtrNDropped = 15,  // rows of non-public partitions seen by k_filter
   kCtrTile0 = 16,  // 16..63 tile claim counters, one per onesweep launch
 };
 
@@ -312,6 +313,11 @@ __global__ __launch_bounds__(kThreads) void k_histogram(const int64_t* __restric
 // K0 (tile form): the same histograms, plus the pass-0 digit count of every
 // 4096-row input tile (tile_cnt[tile][256], u32) for the reduce-then-scan
 // radix pass.  Blocks stride over whole tiles.
+// PID_ONLY (the bucket pass of the L0 pre-filter): the partition column is
+// not read; a row is dropped only for an out-of-range privacy id, and rows of
+// non-public partitions are placed too (k_onesweep<true, true> tags them,
+// k_filter drops them).
+template <bool PID_ONLY>
 __global__ __launch_bounds__(kThreads) void k_histogram_tiles(const int64_t* __restrict__ pid,
                                                               const int64_t* __restrict__ pk, int64_t n,
                                                               KeySpec ks, unsigned long long* __restrict__ hist,
@@ -331,7 +337,8 @@ __global__ __launch_bounds__(kThreads) void k_histogram_tiles(const int64_t* __r
     for (int k = 0; k < kItems; ++k) {
       const int64_t i = base + (int64_t)k * kThreads;
       if (i >= n) break;
-      const int64_t a = pid[i], b = pk[i];
+      const int64_t a = pid[i];
+      const int64_t b = PID_ONLY ? 0 : pk[i];
       if (b < 0 || b >= (int64_t)ks.num_parts || a < 0 || a >= (int64_t)ks.num_pids) {
         if (b >= 0) ++invalid;
         atomicAdd(&sh[256], 1u);
@@ -521,12 +528,25 @@ __global__ __launch_bounds__(kThreads, PDP_OS_OCC) void k_onesweep(
         r[k].pid = (uint32_t)a;
         r[k].pk = (uint32_t)b;
         r[k].val = val ? val[idx] : 0.0;
-        if (b < 0 || b >= (int64_t)ks.num_parts || a < 0 || a >= (int64_t)ks.num_pids)
-          d = 256;  // dropped
-        else
-          d = digit_of(ks, pass, r[k]);
         if constexpr (TAG) {
-          if (d < 256) tg[k] = ((r[k].pid - s_lo[d]) << 5) | filt_level(filt_prio(ks.seed, r[k].pid, r[k].pk));
+          // placed unless the privacy id is out of range (k_histogram_tiles<true>); a non-public row
+          // (pk < 0) is tagged dropped, an out-of-range pk is an error
+          if (a < 0 || a >= (int64_t)ks.num_pids) {
+            d = 256;
+          } else {
+            d = digit_of(ks, pass, r[k]);
+            if (b < 0 || b >= (int64_t)ks.num_parts) {
+              if (b >= 0) atomicAdd(&counters[kCtrInvalid], 1ull);
+              tg[k] = kTagDropped;
+            } else {
+              tg[k] = ((r[k].pid - s_lo[d]) << 5) | filt_level(filt_prio(ks.seed, r[k].pid, r[k].pk));
+            }
+          }
+        } else {
+          if (b < 0 || b >= (int64_t)ks.num_parts || a < 0 || a >= (int64_t)ks.num_pids)
+            d = 256;  // dropped
+          else
+            d = digit_of(ks, pass, r[k]);
         }
       } else {
         r[k] = ld_rec(rin + idx);
@@ -1934,8 +1954,8 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
   {
     ProfScope ps(ctx, PDP_STAGE_HISTOGRAM, stream);
     if (rts)
-      hipLaunchKernelGGL(k_histogram_tiles, dim3(grid_for(L.tiles, 1, 4096)), dim3(kThreads), 0, stream, cols->pid,
-                         cols->pk, n, ks, hist, ts.tile_cnt, counters);
+      hipLaunchKernelGGL(fpl.on ? k_histogram_tiles<true> : k_histogram_tiles<false>, dim3(grid_for(L.tiles, 1, 4096)),
+                         dim3(kThreads), 0, stream, cols->pid, cols->pk, n, ks, hist, ts.tile_cnt, counters);
     else
       hipLaunchKernelGGL(k_histogram<true>, dim3(grid_for(n, kThreads, 2048)), dim3(kThreads), 0, stream,
                          cols->pid, cols->pk, (const Rec*)nullptr, n, ks, hist, counters);
@@ -2084,10 +2104,10 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
   }
   HIP_TRY(hipGetLastError());
 
-  unsigned long long host_ctr[kCtrNSurv + 1];
+  unsigned long long host_ctr[kCtrNDropped + 1];
   HIP_TRY(hipMemcpyAsync(host_ctr, counters, sizeof(host_ctr), hipMemcpyDeviceToHost, stream));
   HIP_TRY(hipStreamSynchronize(stream));
-  ctx->stats.kept_rows_in = (int64_t)host_ctr[kCtrNKept];
+  ctx->stats.kept_rows_in = (int64_t)(host_ctr[kCtrNKept] - host_ctr[kCtrNDropped]);
   n_kept = host_ctr[n_slot];
   for (int i = 0; i < 4; ++i) ctx->stats.sweep_cycles[i] = (int64_t)host_ctr[kCtrSweepCycles + i];
   ctx->stats.sweep_tiles = (int64_t)host_ctr[kCtrSweepTiles];

@@ -153,18 +153,22 @@ def test_full_width_privacy_ids_and_wide_partition_ids(ex):
     assert ex.stats().sort_passes == 4
 
 
-def test_dropped_rows_and_public_partitions(ex):
+@pytest.mark.parametrize("flags", [0, FORCE_FILTER])
+def test_dropped_rows_and_public_partitions(ex, flags):
     n, U, P = 20000, 800, 400
     pid, pk, val = o.synth_rows(n, U, P, seed=9)
     pk = np.where(pk % 3 == 0, -1, pk)  # non-public rows dropped
     bp = o.BoundParams(3, 2, 0.0, 10.0)
-    _, _, rc, cnt, x, _ = run_gpu(ex, pid, pk, val, U, P, bp, 1 | 2 | 16)
+    _, _, rc, cnt, x, _ = run_gpu(ex, pid, pk, val, U, P, bp, 1 | 2 | 16, debug_flags=flags)
+    assert ex.stats().kept_rows_in == int((pk >= 0).sum())
+    assert (ex.stats().filter_rows > 0) == bool(flags)
     ref = o.bound_and_accumulate(pid, pk, val, P, bp, "hash", seed=3)
     check_acc(ref, rc, cnt, x, None, 1 | 2 | 16, val)
     assert rc[::3].sum() == 0
     pk_all = np.full(n, -1)
-    _, _, rc, cnt, x, _ = run_gpu(ex, pid, pk_all, val, U, P, bp, 1 | 2)
+    _, _, rc, cnt, x, _ = run_gpu(ex, pid, pk_all, val, U, P, bp, 1 | 2, debug_flags=flags)
     assert rc.sum() == 0 and cnt.sum() == 0 and np.all(x == 0)
+    assert ex.stats().kept_rows_in == 0
 
 
 def test_empty_input(ex):
@@ -174,13 +178,17 @@ def test_empty_input(ex):
     assert rc.sum() == 0 and cnt.sum() == 0
 
 
-def test_out_of_range_ids_raise(ex):
+@pytest.mark.parametrize("flags", [0, FORCE_FILTER])
+def test_out_of_range_ids_raise(ex, flags):
     from pipelinedp_amd.native import NativeError
     bp = o.BoundParams(1, 1, 0.0, 1.0)
     pid = np.array([0, 1, 2], np.int64)
     pk = np.array([0, 5, 1], np.int64)
     with pytest.raises(NativeError, match="out of range"):
-        run_gpu(ex, pid, pk, np.zeros(3), 3, 5, bp, 1)
+        run_gpu(ex, pid, pk, np.zeros(3), 3, 5, bp, 1, debug_flags=flags)
+    with pytest.raises(NativeError, match="out of range"):
+        run_gpu(ex, np.array([0, 3, 2], np.int64), np.array([0, 4, 1], np.int64), np.zeros(3), 3, 5, bp, 1,
+                debug_flags=flags)
 
 
 def test_already_enforced_matches_oracle(ex):
