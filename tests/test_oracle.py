@@ -154,6 +154,23 @@ def test_hash_sampler_is_uniform():
         assert np.all(np.abs(freq - p) < 4.5 * math.sqrt(p * (1 - p) / trials)), (R, freq)
 
 
+def test_partition_ranking_is_uniform_across_privacy_ids():
+    """For ONE seed, over many privacy ids (the case the hot path sees): each
+    partition is kept with probability L0 / R, each pair with
+    L0 (L0 - 1) / (R (R - 1))."""
+    pids = np.arange(40000)
+    for R, l0 in ((5, 2), (9, 4), (40, 8)):
+        pks = np.tile(np.arange(R) * 7919 + 3, len(pids))
+        pr = o.group_priority(12345, np.repeat(pids, R), pks).reshape(len(pids), R)
+        kept = np.argsort(np.argsort(pr, axis=1, kind="stable"), axis=1, kind="stable") < l0
+        p = l0 / R
+        freq = kept.mean(0)
+        assert np.all(np.abs(freq - p) < 4.5 * math.sqrt(p * (1 - p) / len(pids))), (R, freq)
+        p2 = l0 * (l0 - 1) / (R * (R - 1))
+        f2 = (kept[:, 0] & kept[:, 1]).mean()
+        assert abs(f2 - p2) < 4.5 * math.sqrt(p2 * (1 - p2) / len(pids)), (R, f2, p2)
+
+
 def test_binding_bounds_match_reference_distribution():
     """oracle feistel sampler vs mean of 400 reference LocalBackend runs."""
     d = load("binding_count_sum_pidcount")
