@@ -91,15 +91,16 @@ def parse():
 
 def stage_bytes(stage, n_in, n_kept, P, nfields, survivors=0, survivor_passes=0):
     """Algorithmic bytes of one launch of each kernel (Roofline).
-    With the L0 pre-filter (survivors > 0): the first pass is the bucket pass
-    (+ a 4-B tag per row), k_filter reads the tags twice and moves the
-    survivors' records, and the survivor sort and K2 see the survivors only."""
+    With the L0 pre-filter (survivors > 0): K0 reads the privacy ids only, the
+    first pass is the bucket pass (+ a 4-B tag per row), k_filter reads the
+    tags three times (sketch, count, compaction) and moves the survivors'
+    records, and the survivor sort and K2 see the survivors only."""
     sorted_rows = survivors if survivors else n_kept
     return {
-        "histogram": 16 * n_in,  # read int64 pid + int64 pk
+        "histogram": (8 if survivors else 16) * n_in,  # read int64 pid (+ int64 pk)
         "onesweep_first": (24 + 16 + (4 if survivors else 0)) * n_in,  # read 3 columns, write 16-B records (+ tags)
         "onesweep_rest": 32 * n_kept,  # read + write 16-B records
-        "filter": 8 * n_kept + 32 * survivors,  # tags twice, survivors' records read + written
+        "filter": 12 * n_kept + 32 * survivors,  # tags three times, survivors' records read + written
         # histogram read + per pass (read + write) + per later pass an upsweep read
         "survivor_sort": survivors * (16 + 32 * survivor_passes + 16 * max(survivor_passes - 1, 0)),
         "buckets": 16 * sorted_rows,  # read 16-B records once

@@ -20,7 +20,11 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 STAGE_OF = {"k_histogram": "histogram", "k_segments": "buckets", "k_lean": "buckets", "k_release": "release",
-            "k_histogram_tiles": "histogram", "k_tile_counts": "tile_counts"}
+            "k_histogram_tiles": "histogram", "k_tile_counts": "tile_counts", "k_filter": "filter",
+            "k_thin": "buckets", "k_segments_big": "buckets"}
+# kernels of the radix sort of the L0 pre-filter's survivors (after k_filter)
+SURVIVOR_SORT = {"k_histogram", "k_onesweep", "k_tile_counts", "k_offsets", "k_tile_chunk_sums", "k_tile_chunk_scan",
+                 "k_tile_bases"}
 
 
 def dispatches(path, counter):
@@ -31,17 +35,23 @@ def dispatches(path, counter):
 
 def last_step(rows):
     """Dispatches of the last pipeline step (from the last k_histogram on)."""
-    starts = [i for i, r in enumerate(rows) if r["Kernel_Name"] in ("k_histogram", "k_histogram_tiles")]
+    starts = [i for i, r in enumerate(rows) if r["Kernel_Name"] == "k_histogram_tiles"]
+    if not starts:
+        starts = [i for i, r in enumerate(rows) if r["Kernel_Name"] == "k_histogram"]
     out = rows[starts[-1]:]
     end = next((i for i, r in enumerate(out) if r["Kernel_Name"] == "k_release"), len(out) - 1)
     return out[:end + 1]
 
 
 def stage_bytes(rows, scale):
-    res, seen_sweep = {}, 0
+    res, seen_sweep, filtered = {}, 0, False
     for r in rows:
         name = r["Kernel_Name"]
         b = float(r["Counter_Value"]) * 1024.0 * scale
+        filtered |= name == "k_filter"
+        if filtered and name in SURVIVOR_SORT:
+            res.setdefault("survivor_sort", [0.0])[0] += b  # all kernels of the sort, one launch of the stage
+            continue
         if name == "k_onesweep":
             st = "onesweep_first" if seen_sweep == 0 else "onesweep_rest"
             seen_sweep += 1
