@@ -477,8 +477,12 @@ constexpr int kHalfTile = kTile / PDP_OS_STAGE_DIV;
 constexpr uint32_t kNoPos = 0xFFFFu;
 
 // TAG (the bucket pass of the L0 pre-filter, pdp_filter.inc): also writes,
-// for every kept row, tag = (pid - first pid of its bucket) << 5 | level of
-// its group priority, into tag_out at the row's sorted position.
+// for every placed row, tag = bucket << 21 | (pid - first pid of its bucket)
+// << 5 | level of its group priority (kTagDropped set for a non-public row),
+// into tag_out at the row's sorted position.  The record carries the tag in
+// its pid slot (k_filter rebuilds the pid), so no extra registers or LDS hold
+// it between the load and the scatter (a separate tag array spilled 64 B per
+// lane to scratch: ~8 GB of extra traffic per 1e9 rows).
 template <bool SOA, bool TAG = false>
 __global__ __launch_bounds__(kThreads, PDP_OS_OCC) void k_onesweep(
     const int64_t* __restrict__ pid, const int64_t* __restrict__ pk, const double* __restrict__ val,
@@ -488,7 +492,6 @@ __global__ __launch_bounds__(kThreads, PDP_OS_OCC) void k_onesweep(
     unsigned long long* __restrict__ counters, int tile_slot, const unsigned int* __restrict__ tile_base,
     uint32_t* __restrict__ tag_out, const uint32_t* __restrict__ tag_lo) {
   __shared__ Rec s_rec[kHalfTile];
-  __shared__ uint32_t s_tag[TAG ? kHalfTile : 1];
   __shared__ uint32_t s_lo[TAG ? 256 : 1];
   __shared__ unsigned int s_cnt[4][kHist + 1];
   __shared__ unsigned int s_dstart[256];
@@ -516,7 +519,6 @@ __global__ __launch_bounds__(kThreads, PDP_OS_OCC) void k_onesweep(
 
   Rec r[kItems];
   uint32_t dr[kItems];  // digit (9 bits) | rank in wave << 9; later the sorted position
-  uint32_t tg[TAG ? kItems : 1];
   const int64_t base = tile_start + (int64_t)wave * (kItems * 64) + lane;
 #pragma unroll
   for (int k = 0; k < kItems; ++k) {
@@ -537,9 +539,9 @@ __global__ __launch_bounds__(kThreads, PDP_OS_OCC) void k_onesweep(
             d = digit_of(ks, pass, r[k]);
             if (b < 0 || b >= (int64_t)ks.num_parts) {
               if (b >= 0) atomicAdd(&counters[kCtrInvalid], 1ull);
-              tg[k] = kTagDropped;
+              r[k].pid = kTagDropped | (d << 21);
             } else {
-              tg[k] = ((r[k].pid - s_lo[d]) << 5) | filt_level(filt_prio(ks.seed, r[k].pid, r[k].pk));
+              r[k].pid = (d << 21) | ((r[k].pid - s_lo[d]) << 5) | filt_level(filt_prio(ks.seed, r[k].pid, r[k].pk));
             }
           }
         } else {
@@ -720,10 +722,7 @@ __global__ __launch_bounds__(kThreads, PDP_OS_OCC) void k_onesweep(
 #pragma unroll
     for (int k = 0; k < kItems; ++k) {
       const uint32_t q = dr[k] - h;
-      if (q < (uint32_t)kHalfTile) {
-        s_rec[q] = r[k];
-        if constexpr (TAG) s_tag[q] = tg[k];
-      }
+      if (q < (uint32_t)kHalfTile) s_rec[q] = r[k];
     }
     __syncthreads();
     const unsigned int e = tot - h < (unsigned int)kHalfTile ? tot - h : (unsigned int)kHalfTile;
@@ -732,9 +731,9 @@ __global__ __launch_bounds__(kThreads, PDP_OS_OCC) void k_onesweep(
       if (ks.ablate & kDebugLinearWrite) {
         st_rec(rout + tile_start + (long long)(h + i), rc);
       } else {
-        const long long q = s_gbase[digit_of(ks, pass, rc)] + (long long)(h + i);
+        const long long q = s_gbase[TAG ? (rc.pid >> 21) & 255u : digit_of(ks, pass, rc)] + (long long)(h + i);
         st_rec(rout + q, rc);
-        if constexpr (TAG) tag_out[q] = s_tag[i];
+        if constexpr (TAG) tag_out[q] = rc.pid;
       }
     }
     __syncthreads();
@@ -2009,7 +2008,7 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
     HIP_TRY(hipMemsetAsync(counters + kCtrNSurv, 0, 8, stream));
     {
       ProfScope ps(ctx, PDP_STAGE_FILTER, stream);
-      hipLaunchKernelGGL(k_filter, dim3(256), dim3(kFiltThreads), 0, stream, sorted, tags, spare, off, counters,
+      hipLaunchKernelGGL(k_filter, dim3(256), dim3(kFiltThreads), 0, stream, sorted, tags, tag_lo, spare, off, counters,
                          (int)kCtrNKept, (int)kCtrNSurv, (int)bp->max_partitions_contributed,
                          (sp.debug & kDebugFilterTiming) != 0);
     }
