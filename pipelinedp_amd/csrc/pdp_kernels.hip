@@ -1233,7 +1233,7 @@ int grid_for(int64_t n, int threads, int cap = 4096) {
 }
 
 struct Layout {
-  size_t recs_a, recs_b, recs_c, hist, off, counters, status, ranges, big, tags, tag_lo, total;
+  size_t recs_a, recs_b, recs_c, hist, off, counters, status, ranges, big, tags, tag_lo, keep, total;
   int64_t tiles;
   uint64_t big_cap;
 };
@@ -1255,6 +1255,7 @@ Layout layout_for(int64_t n, bool sweep = false) {
   L.big = o; o += align_up((size_t)L.big_cap * 16, 256);
   L.tags = o; o += sweep ? 0 : align_up((size_t)std::max<int64_t>(n, 1) * 4, 256);  // L0 pre-filter tags
   L.tag_lo = o; o += 256 * 4;
+  L.keep = o; o += sweep ? 0 : align_up((size_t)std::max<int64_t>(n, 1) / 4 + 64, 256);  // k_filter keep bytes
   L.total = o;
   return L;
 }
@@ -2008,7 +2009,8 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
     HIP_TRY(hipMemsetAsync(counters + kCtrNSurv, 0, 8, stream));
     {
       ProfScope ps(ctx, PDP_STAGE_FILTER, stream);
-      hipLaunchKernelGGL(k_filter, dim3(256), dim3(kFiltThreads), 0, stream, sorted, tags, tag_lo, spare, off, counters,
+      hipLaunchKernelGGL(k_filter, dim3(256), dim3(kFiltThreads), 0, stream, sorted, tags, tag_lo, spare,
+                         (uint8_t*)(ws + L.keep), off, counters,
                          (int)kCtrNKept, (int)kCtrNSurv, (int)bp->max_partitions_contributed,
                          (sp.debug & kDebugFilterTiming) != 0);
     }
