@@ -2019,7 +2019,11 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
     HIP_TRY(hipMemcpyAsync(&m, counters + kCtrNSurv, 8, hipMemcpyDeviceToHost, stream));
     HIP_TRY(hipStreamSynchronize(stream));
     ctx->stats.filter_rows = (int64_t)m;
-    // survivors by (bucket, pid & (2^low_bits - 1)): groups every pid (a bucket spans <= 2^low_bits ids)
+    // Survivors stably by pid & (2^low_bits - 1) only.  That groups every pid: within a bucket the
+    // ids are distinct mod 2^low_bits (a bucket spans <= 2^low_bits ids), and rows of equal low bits
+    // from different buckets stay in the order of their buckets' runs, because k_filter writes each
+    // bucket's survivors as ONE contiguous run.  (No bucket-digit pass: the order of the pids does
+    // not matter to K2, only their grouping.)
     KeySpec k2 = ks;
     k2.passes = 0;
     for (int sh = 0; sh < fpl.low_bits; sh += 8) {
@@ -2027,9 +2031,6 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
       k2.bits[k2.passes] = std::min(8, fpl.low_bits - sh);
       ++k2.passes;
     }
-    k2.shift[k2.passes] = 64;
-    k2.bits[k2.passes] = 8;
-    ++k2.passes;
     ctx->stats.sort_passes += k2.passes;
     if (m == 0) HIP_TRY(hipMemsetAsync(counters + kCtrNGeneric, 0, 8, stream));
     Rec* sa = spare;

@@ -112,19 +112,22 @@ def test_bound_accumulate_matches_oracle(ex, cfgi, mode):
             assert st.filter_rows <= n
 
 
-@pytest.mark.parametrize("L0,Linf,z", [(1, 1, 1.1), (2, 3, 0.0), (4, 2, 1.1), (8, 4, 0.0), (8, 1, 1.3)])
-def test_prefilter_matches_unfiltered_at_scale(ex, L0, Linf, z):
-    """The L0 pre-filter (automatic at this size: 2^22 rows, 100 rows per
-    privacy id) against the same run with the filter disabled, and both
-    against the oracle: counts and privacy-id counts bit-exact, sums to
-    1e-9; the survivors are a small share of the rows."""
-    n, U, P = 1 << 22, (1 << 22) // 100, 200000
+@pytest.mark.parametrize("L0,Linf,z,rows_per_pid", [(1, 1, 1.1, 100), (2, 3, 0.0, 100), (4, 2, 1.1, 100),
+                                                    (8, 4, 0.0, 100), (8, 1, 1.3, 100), (2, 2, 1.1, 14)])
+def test_prefilter_matches_unfiltered_at_scale(ex, L0, Linf, z, rows_per_pid):
+    """The L0 pre-filter (automatic at this size: 2^22 rows) against the same
+    run with the filter disabled, and both against the oracle: counts and
+    privacy-id counts bit-exact, sums to 1e-9; the survivors are a small
+    share of the rows.  With 14 rows per pid, U ~ 3e5 > 2^16: privacy ids of
+    different buckets share their low 16 bits, the survivor sort's key."""
+    n, P = 1 << 22, 200000
+    U = n // rows_per_pid
     pid, pk, val = o.synth_rows(n, U, P, seed=500 + L0, zipf_s=z, value_lo=-5, value_hi=15)
     bp = o.BoundParams(L0, Linf, 0.0, 10.0)
     mask = 1 | 2 | 4 | 16
     _, _, rc, cnt, x, _ = run_gpu(ex, pid, pk, val, U, P, bp, mask, seed=9)
     surv = ex.stats().filter_rows
-    assert 0 < surv < n // 2
+    assert 0 < surv < (n // 2 if rows_per_pid >= 100 else n)
     _, _, rc2, cnt2, x2, _ = run_gpu(ex, pid, pk, val, U, P, bp, mask, seed=9, debug_flags=NO_FILTER)
     assert ex.stats().filter_rows == 0
     np.testing.assert_array_equal(rc, rc2)
