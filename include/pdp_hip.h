@@ -163,7 +163,11 @@ void pdp_ctx_destroy(pdp_ctx* ctx);
 /* Bytes of device workspace pdp_bound_accumulate needs for these columns. */
 int pdp_workspace_size(const pdp_columns* cols, const pdp_bound_params* bp, size_t* bytes);
 
-/* Rows -> dense per-partition accumulators (zeroed first). */
+/* Rows -> dense per-partition accumulators (zeroed first).  For L0 <= 8 with
+ * enough rows per privacy id the library first drops, after one bucket
+ * radix pass, the rows of partitions their privacy id cannot keep (the L0
+ * pre-filter); the result is identical either way, and
+ * pdp_get_stats reports the surviving rows in filter_rows. */
 int pdp_bound_accumulate(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp,
                          const pdp_accumulators* acc, void* workspace, size_t workspace_bytes,
                          void* stream);
