@@ -441,6 +441,49 @@ def _group_starts(keys_sorted_list):
     return start
 
 
+def _bit_length32(h):
+    """Bit length of uint64 arrays holding 32-bit values (0 for 0)."""
+    h = _u64(h).copy()
+    n = np.zeros(h.shape, dtype=np.int64)
+    for sh in (16, 8, 4, 2, 1):
+        big = h >= (np.uint64(1) << np.uint64(sh))
+        n[big] += sh
+        h[big] >>= np.uint64(sh)
+    return n + (h > 0)
+
+
+def prefilter_level(h):
+    """Level of a 32-bit group priority h on a log scale with 4 levels per
+    octave, 0..31 (pdp_filter.inc:filt_level): 4 (7 - e) + #{thresholds
+    2^(k/4) 2^31 <= mantissa}, e = leading zeros of h; 0 when e >= 8."""
+    h = _u64(h) & _M32
+    e = 32 - _bit_length32(h)
+    m = (h << np.minimum(e, 31).astype(np.uint64)) & _M32
+    f = (m >= np.uint64(0x9837F052)).astype(np.int64) + (m >= np.uint64(0xB504F334)) + (m >= np.uint64(0xD744FCCB))
+    return np.where(e >= 8, 0, 4 * (7 - e) + f)
+
+
+def prefilter_survivors(pid, pk, seed, l0):
+    """Restatement of the L0 pre-filter (pdp_filter.inc) for
+    checking: per privacy id a 32-bit sketch with bit level(top32(group
+    priority)) set for each of its rows; K = level of the L0-th set bit (31
+    when fewer); a row survives iff its level <= K.  Rows with pk < 0 never
+    survive.  (The GPU groups privacy ids into buckets first; that changes
+    nothing per privacy id.)  Returns the boolean survivor mask."""
+    pid = np.asarray(pid, dtype=np.int64)
+    pk = np.asarray(pk, dtype=np.int64)
+    ok = pk >= 0
+    lvl = np.zeros(len(pid), dtype=np.int64)
+    lvl[ok] = prefilter_level(group_priority(seed, pid[ok], pk[ok]) >> np.uint64(32))
+    uniq, inv = np.unique(pid, return_inverse=True)
+    sketch = np.zeros(len(uniq), dtype=np.uint64)
+    np.bitwise_or.at(sketch, inv[ok], np.left_shift(np.uint64(1), lvl[ok].astype(np.uint64)))
+    bits = ((sketch[:, None] >> np.arange(32, dtype=np.uint64)) & np.uint64(1)).astype(np.int64)
+    cs = np.cumsum(bits, axis=1)
+    K = np.where(cs[:, -1] >= l0, np.argmax(cs >= l0, axis=1), 31)
+    return ok & (lvl <= K[inv])
+
+
 def bound_and_accumulate(pid, pk, value, num_partitions, params: BoundParams,
                          sampler="hash", seed=0, rng=None) -> Accumulators:
     """SamplingCrossAndPerPartitionContributionBounder.bound_contributions

@@ -108,8 +108,8 @@ def test_bound_accumulate_matches_oracle(ex, cfgi, mode):
         assert st.fallback_rows > 0  # huge privacy ids went through the generic path
     if mode.startswith("filter"):
         assert (st.filter_rows > 0) == (L0 <= FILTER_MAX_L0)  # the pre-filter ran (and kept rows)
-        if L0 <= FILTER_MAX_L0:
-            assert st.filter_rows <= n
+        if L0 <= FILTER_MAX_L0:  # exactly the restated filter's survivors (pdp_oracle.prefilter_survivors)
+            assert st.filter_rows == int(o.prefilter_survivors(pid, pk, 77 + cfgi, L0).sum())
 
 
 @pytest.mark.parametrize("L0,Linf,z,rows_per_pid", [(1, 1, 1.1, 100), (2, 3, 0.0, 100), (4, 2, 1.1, 100),
@@ -128,6 +128,7 @@ def test_prefilter_matches_unfiltered_at_scale(ex, L0, Linf, z, rows_per_pid):
     _, _, rc, cnt, x, _ = run_gpu(ex, pid, pk, val, U, P, bp, mask, seed=9)
     surv = ex.stats().filter_rows
     assert 0 < surv < (n // 2 if rows_per_pid >= 100 else n)
+    assert surv == int(o.prefilter_survivors(pid, pk, 9, L0).sum())  # the restated filter, row for row
     _, _, rc2, cnt2, x2, _ = run_gpu(ex, pid, pk, val, U, P, bp, mask, seed=9, debug_flags=NO_FILTER)
     assert ex.stats().filter_rows == 0
     np.testing.assert_array_equal(rc, rc2)

@@ -230,3 +230,33 @@ def test_select_partitions_binding_matches_reference_distribution():
     p = (freq + d["freq"]) / 2
     sd = np.sqrt(2 * p * (1 - p) / runs) + 1e-9
     assert np.all(np.abs(freq - d["freq"]) <= 4.5 * sd), (freq, d["freq"])
+
+
+@pytest.mark.parametrize("n,U,P,z,L0,Linf", [(200000, 2000, 5000, 1.1, 4, 2), (150000, 1500, 800, 0.0, 8, 4),
+                                            (100000, 1000, 20000, 1.3, 1, 1), (50000, 10000, 300, 1.1, 2, 3)])
+def test_prefilter_drops_only_rows_the_bounding_drops(n, U, P, z, L0, Linf):
+    """The L0 pre-filter restated (pdp_oracle.prefilter_survivors): bounding
+    the survivors gives exactly the accumulators of bounding every row, and
+    for enough rows per privacy id most rows are dropped."""
+    pid, pk, val = o.synth_rows(n, U, P, seed=77, zipf_s=z)
+    pk = np.where((pid % 11) == 0, -1, pk)  # some non-public rows
+    bp = o.BoundParams(L0, Linf, 0.0, 10.0)
+    surv = o.prefilter_survivors(pid, pk, 5, L0)
+    full = o.bound_and_accumulate(pid, pk, val, P, bp, "hash", seed=5)
+    part = o.bound_and_accumulate(pid[surv], pk[surv], val[surv], P, bp, "hash", seed=5)
+    np.testing.assert_array_equal(full.row_count, part.row_count)
+    np.testing.assert_array_equal(full.count, part.count)
+    np.testing.assert_allclose(full.nsum, part.nsum, rtol=1e-12, atol=1e-9)
+    assert not surv[pk < 0].any()
+    if n // U >= 16 * L0:
+        assert surv.mean() < 0.5
+
+
+def test_prefilter_level_is_monotone_and_covers_32_levels():
+    h = np.array([0, 1, (1 << 24) - 1, 1 << 24, 0x01306FE1, 1 << 25, 1 << 31, 0x9837F051 << 0, 0xD744FCCB,
+                  0xFFFFFFFF], dtype=np.uint64)
+    lv = o.prefilter_level(np.sort(h))
+    assert np.all(np.diff(lv) >= 0) and lv[0] == 0 and lv[-1] == 31
+    x = np.sort(np.random.default_rng(1).integers(0, 1 << 32, 100000, dtype=np.uint64))
+    lx = o.prefilter_level(x)
+    assert np.all(np.diff(lx) >= 0) and set(np.unique(lx)) <= set(range(32))
