@@ -77,6 +77,8 @@ CONFIGS = [
     (40000, 400, 40, 1.1, 16, 2, (0.0, 10.0), None, 1 | 2 | 4 | 16),  # sorted K2 + second (L_inf) sort
     (20000, 400, 12, 0.0, 17, 3, (-1.0, 4.0), None, 1 | 4 | 8),  # sorted K2, every group over L_inf
     (12000, 200, 500, 1.1, 70, 1, (0.0, 10.0), None, 1 | 2 | 16),  # sorted K2 with two output slots
+    (40000, 300, 500, 1.1, 3, 12, (0.0, 10.0), None, 1 | 2 | 4 | 8 | 16),  # pre-filter with L_inf > 8: k_lean
+    (60000, 150, 2000, 1.2, 8, 8, (-1.0, 6.0), (-2.0, 30.0), 1 | 2),  # largest thin L0 / L_inf, sum bounds
 ]
 
 
