@@ -463,24 +463,42 @@ def prefilter_level(h):
     return np.where(e >= 8, 0, 4 * (7 - e) + f)
 
 
-def prefilter_survivors(pid, pk, seed, l0):
+PREFILTER_WORDS = 39936  # LDS sketch words per bucket (pdp_filter.inc kFiltWords)
+
+
+def prefilter_sketch_bits(num_privacy_ids):
+    """Sketch width the GPU uses for U privacy ids (pdp_kernels.hip
+    filter_plan): 256 buckets of pids with (pid * mult) >> 32 = b,
+    mult = floor(2^40 / U); 32 bits per pid when the widest bucket has <=
+    PREFILTER_WORDS pids, 16 bits up to twice that, else no filter (0)."""
+    U = int(num_privacy_ids)
+    mult = (1 << 40) // U
+    lo = [((b << 32) + mult - 1) // mult for b in range(257)]
+    width = max(min(lo[b + 1], U) - lo[b] for b in range(256))
+    return 32 if width <= PREFILTER_WORDS else (16 if width <= 2 * PREFILTER_WORDS else 0)
+
+
+def prefilter_survivors(pid, pk, seed, l0, sketch_bits=32):
     """Restatement of the L0 pre-filter (pdp_filter.inc) for
-    checking: per privacy id a 32-bit sketch with bit level(top32(group
-    priority)) set for each of its rows; K = level of the L0-th set bit (31
-    when fewer); a row survives iff its level <= K.  Rows with pk < 0 never
-    survive.  (The GPU groups privacy ids into buckets first; that changes
-    nothing per privacy id.)  Returns the boolean survivor mask."""
+    checking: per privacy id a sketch with bit level(top32(group priority))
+    set for each of its rows; K = level of the L0-th set bit (the top level
+    when fewer); a row survives iff its level <= K.  With 16-bit sketches
+    (buckets wider than PREFILTER_WORDS pids) levels are halved.  Rows with
+    pk < 0 never survive.  (The GPU groups privacy ids into buckets first;
+    that changes nothing per privacy id.)  Returns the boolean survivor mask."""
     pid = np.asarray(pid, dtype=np.int64)
     pk = np.asarray(pk, dtype=np.int64)
     ok = pk >= 0
     lvl = np.zeros(len(pid), dtype=np.int64)
     lvl[ok] = prefilter_level(group_priority(seed, pid[ok], pk[ok]) >> np.uint64(32))
+    if sketch_bits == 16:
+        lvl = lvl >> 1
     uniq, inv = np.unique(pid, return_inverse=True)
     sketch = np.zeros(len(uniq), dtype=np.uint64)
     np.bitwise_or.at(sketch, inv[ok], np.left_shift(np.uint64(1), lvl[ok].astype(np.uint64)))
-    bits = ((sketch[:, None] >> np.arange(32, dtype=np.uint64)) & np.uint64(1)).astype(np.int64)
+    bits = ((sketch[:, None] >> np.arange(sketch_bits, dtype=np.uint64)) & np.uint64(1)).astype(np.int64)
     cs = np.cumsum(bits, axis=1)
-    K = np.where(cs[:, -1] >= l0, np.argmax(cs >= l0, axis=1), 31)
+    K = np.where(cs[:, -1] >= l0, np.argmax(cs >= l0, axis=1), sketch_bits - 1)
     return ok & (lvl <= K[inv])
 
 

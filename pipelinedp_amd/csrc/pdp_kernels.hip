@@ -477,7 +477,7 @@ constexpr int kHalfTile = kTile / PDP_OS_STAGE_DIV;
 constexpr uint32_t kNoPos = 0xFFFFu;
 
 // TAG (the bucket pass of the L0 pre-filter, pdp_filter.inc): also writes,
-// for every placed row, tag = bucket << 21 | (pid - first pid of its bucket)
+// for every placed row, tag = bucket << 22 | (pid - first pid of its bucket)
 // << 5 | level of its group priority (kTagDropped set for a non-public row),
 // into tag_out at the row's sorted position.  The record carries the tag in
 // its pid slot (k_filter rebuilds the pid), so no extra registers or LDS hold
@@ -539,9 +539,9 @@ __global__ __launch_bounds__(kThreads, PDP_OS_OCC) void k_onesweep(
             d = digit_of(ks, pass, r[k]);
             if (b < 0 || b >= (int64_t)ks.num_parts) {
               if (b >= 0) atomicAdd(&counters[kCtrInvalid], 1ull);
-              r[k].pid = kTagDropped | (d << 21);
+              r[k].pid = kTagDropped | (d << 22);
             } else {
-              r[k].pid = (d << 21) | ((r[k].pid - s_lo[d]) << 5) | filt_level(filt_prio(ks.seed, r[k].pid, r[k].pk));
+              r[k].pid = (d << 22) | ((r[k].pid - s_lo[d]) << 5) | filt_level(filt_prio(ks.seed, r[k].pid, r[k].pk));
             }
           }
         } else {
@@ -731,7 +731,7 @@ __global__ __launch_bounds__(kThreads, PDP_OS_OCC) void k_onesweep(
       if (ks.ablate & kDebugLinearWrite) {
         st_rec(rout + tile_start + (long long)(h + i), rc);
       } else {
-        const long long q = s_gbase[TAG ? (rc.pid >> 21) & 255u : digit_of(ks, pass, rc)] + (long long)(h + i);
+        const long long q = s_gbase[TAG ? (rc.pid >> 22) & 255u : digit_of(ks, pass, rc)] + (long long)(h + i);
         st_rec(rout + q, rc);
         if constexpr (TAG) tag_out[q] = rc.pid;
       }
@@ -1806,9 +1806,11 @@ namespace {
 
 // When the L0 pre-filter runs (pdp_filter.inc): small L0, enough rows per
 // privacy id for most of them to fall outside the kept partitions, and
-// buckets of at most kFiltWords privacy ids.
+// buckets of at most 2 x kFiltWords privacy ids (U up to ~20e6; beyond
+// kFiltWords per bucket the sketch is 16 bits per pid).
 struct FilterPlan {
   bool on;
+  bool half;      // buckets of up to 2 x kFiltWords pids: two 16-bit sketches per LDS word
   uint64_t mult;  // bucket digit = (pid * mult) >> 32
   int low_bits;   // pid bits that tell the ids of one bucket apart
 };
@@ -1831,8 +1833,9 @@ FilterPlan filter_plan(int64_t n, int64_t U, const pdp_bound_params* bp, int deb
     const uint64_t hi = std::min<uint64_t>(filt_bucket_lo(b + 1, mult), (uint64_t)U);
     if (hi > lo) width = std::max(width, hi - lo);
   }
-  if (width > (uint64_t)kFiltWords) return f;
+  if (width > 2ull * kFiltWords) return f;
   f.on = true;
+  f.half = width > (uint64_t)kFiltWords;
   f.mult = mult;
   f.low_bits = std::max(1, pdp::ceil_log2_u64(width));
   return f;
@@ -2009,7 +2012,8 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
     HIP_TRY(hipMemsetAsync(counters + kCtrNSurv, 0, 8, stream));
     {
       ProfScope ps(ctx, PDP_STAGE_FILTER, stream);
-      hipLaunchKernelGGL(k_filter, dim3(256), dim3(kFiltThreads), 0, stream, sorted, tags, tag_lo, spare,
+      hipLaunchKernelGGL(fpl.half ? k_filter<true> : k_filter<false>, dim3(256), dim3(kFiltThreads), 0, stream,
+                         sorted, tags, tag_lo, spare,
                          (uint8_t*)(ws + L.keep), off, counters,
                          (int)kCtrNKept, (int)kCtrNSurv, (int)bp->max_partitions_contributed,
                          (sp.debug & kDebugFilterTiming) != 0);

@@ -159,6 +159,29 @@ def test_full_width_privacy_ids_and_wide_partition_ids(ex):
     assert ex.stats().sort_passes == 4
 
 
+@pytest.mark.parametrize("L0,Linf", [(1, 1), (4, 2), (8, 3)])
+def test_prefilter_half_sketch_wide_buckets(ex, L0, Linf):
+    """U = 1.5e7 privacy ids: buckets of ~58,600 ids, wider than the LDS
+    holds at 32 bits per id, so the filter uses 16-bit sketches (2 levels
+    per octave).  20,000 ids spread over the whole range carry ~100 rows
+    each.  Survivors equal the restatement's; bounding equals the oracle."""
+    rng = np.random.default_rng(11 + L0)
+    U, P, n = 15_000_000, 50_000, 1 << 21
+    assert o.prefilter_sketch_bits(U) == 16
+    ids = rng.choice(U, 20000, replace=False)
+    pid = ids[rng.integers(0, len(ids), n)].astype(np.int64)
+    pk = np.minimum(rng.zipf(1.3, n) - 1, P - 1).astype(np.int64)
+    val = rng.uniform(-5, 15, n)
+    bp = o.BoundParams(L0, Linf, 0.0, 10.0)
+    mask = 1 | 2 | 4 | 16
+    _, _, rc, cnt, x, _ = run_gpu(ex, pid, pk, val, U, P, bp, mask, seed=21, debug_flags=FORCE_FILTER)
+    surv = ex.stats().filter_rows
+    assert surv == int(o.prefilter_survivors(pid, pk, 21, L0, 16).sum())
+    assert surv < n
+    ref = o.bound_and_accumulate(pid, pk, val, P, bp, "hash", seed=21)
+    check_acc(ref, rc, cnt, x, None, mask, val)
+
+
 @pytest.mark.parametrize("flags", [0, FORCE_FILTER])
 def test_dropped_rows_and_public_partitions(ex, flags):
     n, U, P = 20000, 800, 400

@@ -232,16 +232,17 @@ def test_select_partitions_binding_matches_reference_distribution():
     assert np.all(np.abs(freq - d["freq"]) <= 4.5 * sd), (freq, d["freq"])
 
 
+@pytest.mark.parametrize("bits", [32, 16])
 @pytest.mark.parametrize("n,U,P,z,L0,Linf", [(200000, 2000, 5000, 1.1, 4, 2), (150000, 1500, 800, 0.0, 8, 4),
                                             (100000, 1000, 20000, 1.3, 1, 1), (50000, 10000, 300, 1.1, 2, 3)])
-def test_prefilter_drops_only_rows_the_bounding_drops(n, U, P, z, L0, Linf):
+def test_prefilter_drops_only_rows_the_bounding_drops(n, U, P, z, L0, Linf, bits):
     """The L0 pre-filter restated (pdp_oracle.prefilter_survivors): bounding
     the survivors gives exactly the accumulators of bounding every row, and
     for enough rows per privacy id most rows are dropped."""
     pid, pk, val = o.synth_rows(n, U, P, seed=77, zipf_s=z)
     pk = np.where((pid % 11) == 0, -1, pk)  # some non-public rows
     bp = o.BoundParams(L0, Linf, 0.0, 10.0)
-    surv = o.prefilter_survivors(pid, pk, 5, L0)
+    surv = o.prefilter_survivors(pid, pk, 5, L0, bits)
     full = o.bound_and_accumulate(pid, pk, val, P, bp, "hash", seed=5)
     part = o.bound_and_accumulate(pid[surv], pk[surv], val[surv], P, bp, "hash", seed=5)
     np.testing.assert_array_equal(full.row_count, part.row_count)
@@ -260,3 +261,9 @@ def test_prefilter_level_is_monotone_and_covers_32_levels():
     x = np.sort(np.random.default_rng(1).integers(0, 1 << 32, 100000, dtype=np.uint64))
     lx = o.prefilter_level(x)
     assert np.all(np.diff(lx) >= 0) and set(np.unique(lx)) <= set(range(32))
+
+
+def test_prefilter_sketch_width_rule():
+    assert o.prefilter_sketch_bits(10_000_000) == 32  # c3: 39,063 pids per bucket
+    assert o.prefilter_sketch_bits(15_000_000) == 16
+    assert o.prefilter_sketch_bits(30_000_000) == 0
