@@ -4,11 +4,18 @@ selection (BASELINE.json metric) on synthetic Zipf(1.1)-keyed rows.
   python bench.py [--gpus N --steps K --warmup W]
 
 One "step" = one pass of the hot path over one batch: pdp_bound_accumulate
-(histogram + radix passes + LDS bucket bounding/accumulation) [+ RCCL
-reduce-scatter of the per-partition accumulators when N > 1] + pdp_release
-(truncated-geometric selection + Laplace noise).  Inputs (int64 pid, int64
-pk, f64 value) are generated on device before timing and stay resident.
-Weak scaling: every rank processes --rows rows of its own privacy ids.
+(histogram + radix passes + LDS bucket bounding + K4 per-partition reduction)
+[+ RCCL reduce-scatter of the per-partition accumulators when N > 1] +
+pdp_release (truncated-geometric selection + Laplace noise).  Inputs (int64
+pid, int64 pk, f64 value) are generated on device before timing and stay
+resident.
+
+Scaling.  c3 is BASELINE.json's headline "1B rows/1M partitions" across the
+node: with --gpus N every rank processes 1e9/N rows of 1e7/N privacy ids of
+its own (pid-sharded input, strong scaling; the N=1 line is the whole 1e9
+rows on one GPU).  --weak keeps --rows rows per rank instead.  c4 is one
+GPU's share of the 8-GPU stress config (4e9 rows total, 5e8 per GPU): weak
+at every N.
 """
 import argparse
 import json
@@ -25,9 +32,10 @@ PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 # c3 is the headline: COUNT+SUM+MEAN, private selection, 1e9 rows / 1e6 Zipf partitions.
 # c2: COUNT+SUM over 1e5 PUBLIC partitions (no selection), 1e8 rows, 1e6 uniform pids.
 # c4: high-cardinality stress, one GPU's shard of 4e9 rows / 5e7 Zipf partitions, L0=32.
+# `strong`: --rows / --pids are node totals split over the ranks (c3 = 1e9 rows across the node).
 WORKLOADS = {
     "c3": dict(rows=1e9, partitions=1e6, pids=1e7, zipf=1.1, l0=4, linf=2, public=False, metrics="mean",
-               cpu_sample=6e6),  # CPU baseline rows per host core
+               cpu_sample=6e6, strong=True),  # CPU baseline rows per host core
     "c2": dict(rows=1e8, partitions=1e5, pids=1e6, zipf=0.0, l0=8, linf=4, public=True, metrics="count_sum",
                cpu_sample=6e6),
     "c4": dict(rows=5e8, partitions=5e7, pids=1.25e7, zipf=1.1, l0=32, linf=4, public=False, metrics="mean",
@@ -82,20 +90,27 @@ def parse():
     p.add_argument("--no-profile", action="store_true")
     p.add_argument("--seed", type=int, default=20250204)
     p.add_argument("--debug-flags", type=int, default=0, help="kernel ablation flags (experiments only)")
+    p.add_argument("--weak", action="store_true", help="c3: --rows / --pids per rank instead of node totals")
     args = p.parse_args()
     for k, v in WORKLOADS[args.workload].items():
-        if getattr(args, k, None) is None:
+        if k != "strong" and getattr(args, k, None) is None:
             setattr(args, k, v)
+    args.strong = bool(WORKLOADS[args.workload].get("strong")) and not args.weak
     return args
 
 
-def stage_bytes(stage, n_in, n_kept, P, nfields, survivors=0, survivor_passes=0):
+def stage_bytes(stage, n_in, n_kept, P, nfields, survivors=0, survivor_passes=0, k4=None):
     """Algorithmic bytes of one launch of each kernel (Roofline).
     With the L0 pre-filter (survivors > 0): K0 reads the privacy ids only, the
     first pass is the bucket pass (+ a 4-B tag per row), k_filter reads the
     tags three times (sketch, count, compaction) and moves the survivors'
-    records, and the survivor sort and K2 see the survivors only."""
+    records, and the survivor sort and K2 see the survivors only.  K4
+    (k4 = (slots, pairs, passes)): K2 also writes one 16-B slot per sorted row,
+    the first pair pass reads the slots and writes the pairs, later passes
+    read + write the pairs, the reduction reads the pairs and writes
+    row_count / count / x (8 B each) per partition."""
     sorted_rows = survivors if survivors else n_kept
+    slots, pairs, kpasses = k4 or (0, 0, 0)
     return {
         "histogram": (8 if survivors else 16) * n_in,  # read int64 pid (+ int64 pk)
         "onesweep_first": (24 + 16 + (4 if survivors else 0)) * n_in,  # read 3 columns, write 16-B records (+ tags)
@@ -103,7 +118,9 @@ def stage_bytes(stage, n_in, n_kept, P, nfields, survivors=0, survivor_passes=0)
         "filter": 12 * n_kept + 32 * survivors,  # tags three times, survivors' records read + written
         # histogram read + per pass (read + write) + per later pass an upsweep read
         "survivor_sort": survivors * (16 + 32 * survivor_passes + 16 * max(survivor_passes - 1, 0)),
-        "buckets": 16 * sorted_rows,  # read 16-B records once
+        "buckets": 16 * sorted_rows + 16 * slots,  # read 16-B records once (+ K4: write the pair slots)
+        "pair_pass": 16 * slots + 16 * pairs + 32 * pairs * max(kpasses - 1, 0),
+        "reduce": 16 * pairs + 24 * P,
         "release": P * (3 * 8 + 1 + 8 * nfields),
         # c5: read the input columns once; read the (pk, privacy id, count, sum) pairs once and write
         # C x P x (3 metrics x 5 + keep probability) doubles
@@ -112,18 +129,29 @@ def stage_bytes(stage, n_in, n_kept, P, nfields, survivors=0, survivor_passes=0)
     }.get(stage)
 
 
-def copy_peak_gbs(torch, nbytes=8 << 30, iters=5):
-    """Achievable HBM ceiling on this box: a device-to-device copy of
-    `nbytes` (read + write bytes / time), the measured counterpart of the
-    8 TB/s spec peak."""
+def copy_peak_gbs(torch, lib=None, nbytes=8 << 30, iters=5):
+    """Achievable HBM ceiling on this box (read + write bytes / time of a
+    device-to-device copy of `nbytes`), the measured counterpart of the 8 TB/s
+    spec peak: with `lib`, libpdp_hip's 16-B-per-lane
+    streaming kernel (pdp_stream_copy, the float4 shape MI355X_MICROARCH.md
+    measures at 6.29 TB/s); else torch's copy_."""
+    import ctypes
     src = torch.empty(nbytes // 8, dtype=torch.int64, device="cuda")
     dst = torch.empty_like(src)
-    dst.copy_(src)
+    stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+    def copy():
+        if lib is None:
+            dst.copy_(src)
+        elif lib.pdp_stream_copy(ctypes.c_void_p(src.data_ptr()), ctypes.c_void_p(dst.data_ptr()), nbytes, stream):
+            raise RuntimeError("pdp_stream_copy failed")
+
+    copy()
     torch.cuda.synchronize()
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     a.record()
     for _ in range(iters):
-        dst.copy_(src)
+        copy()
     b.record()
     torch.cuda.synchronize()
     gbs = 2 * nbytes * iters / (a.elapsed_time(b) * 1e-3) / 1e9
@@ -305,13 +333,13 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         world = World(rank, world_size)
 
-    n = int(args.rows)
+    n = int(args.rows // world_size) if args.strong else int(args.rows)
     P = int(args.partitions)
-    U = int(args.pids)
+    U = int(args.pids // world_size) if args.strong else int(args.pids)
     ex = HipExecutor(local)
     pid, pk, val = ex.generate(n, U, P, seed=args.seed, zipf_s=args.zipf, lo=0.0, hi=10.0, row_offset=rank * n)
     # Multi-GPU: rank r's rows carry its own privacy ids (global id = r * U + local id), so every privacy id
-    # lives on one rank (pid-sharded input, weak scaling); the sort uses the dense local ids.
+    # lives on one rank (pid-sharded input); the sort uses the dense local ids.
     public = WORKLOADS[args.workload]["public"]
     count_sum = WORKLOADS[args.workload]["metrics"] == "count_sum"
     sweep = WORKLOADS[args.workload]["metrics"] == "analysis"
@@ -353,6 +381,7 @@ def main():
     rows_after_public_filter = int(st.kept_rows_in)
     surv = int(st.filter_rows)  # rows that survive the L0 pre-filter (0: it did not run)
     surv_passes = int(st.sort_passes) - 1 if surv else 0
+    k4 = (int(st.k4_slots), int(st.k4_pairs), int(st.k4_passes)) if st.k4_slots else None
     if not args.no_profile:
         ex.profile(True)
         ex.profile_read(reset=True)
@@ -382,7 +411,7 @@ def main():
                 stages[s] = {"ms_per_launch": ms / cnt, "launches_per_step": cnt / args.steps}
         dom = max(stages, key=lambda s: stages[s]["ms_per_launch"] * stages[s]["launches_per_step"])
         nb = (P + world_size - 1) // world_size if world else P
-        b = stage_bytes(dom, n, rows_after_public_filter, nb, len(fields), surv, surv_passes)
+        b = stage_bytes(dom, n, rows_after_public_filter, nb, len(fields), surv, surv_passes, k4)
         ach = b / (stages[dom]["ms_per_launch"] * 1e-3) / 1e9
         traffic, prof_round = pmc_traffic(dom, n) if not sweep else (None, None)
         roofline = {"bound": "hbm", "kernel": dom, "achieved": round(ach, 1), "peak": PEAK_HBM_GBS,
@@ -399,7 +428,7 @@ def main():
                                       "completeness only"} if sweep else {}),
                     "ms_per_launch_source": "hipEvents on the launch stream, averaged over the timed steps"}
         for s in stages:
-            bs = stage_bytes(s, n, rows_after_public_filter, nb, len(fields), surv, surv_passes)
+            bs = stage_bytes(s, n, rows_after_public_filter, nb, len(fields), surv, surv_passes, k4)
             if bs:
                 stages[s]["achieved_GBs"] = round(bs / (stages[s]["ms_per_launch"] * 1e-3) / 1e9, 1)
 
@@ -412,16 +441,18 @@ def main():
         del acc
 
     rows_per_s = n * world_size * args.steps / elapsed
-    copy_gbs = copy_peak_gbs(torch) if rank == 0 and not args.no_profile else None
+    copy_gbs = copy_peak_gbs(torch, native.lib()) if rank == 0 and not args.no_profile else None
     if roofline is not None:
         roofline["copy_peak_measured"] = copy_gbs
+        roofline["copy_peak_note"] = ("pdp_stream_copy: 16-B-per-lane streaming copy of 8 GiB, (read + write) bytes / "
+                                      "time; the achievable ceiling next to the 8 TB/s spec peak")
     if rank == 0:
         e2e = rows_per_s * 24 / 1e9
         line = {
             "metric": "input rows/sec (node) for DP COUNT+SUM+MEAN, 1B rows/1M partitions; % HBM peak",
             "value": rows_per_s, "unit": "rows/s", "n_gpus": world_size, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+            "scaling": "strong" if args.strong else "weak", "vs_baseline": None, "dtype": "f64",
             "data": "synthetic (on-device Philox generator, oracle/pdp_oracle.py:synth_rows)",
             "config": {"workload": (f"c5: UtilityAnalysisEngine.analyze, {len(SWEEP)} configurations "
                                     f"(L0 1..128 x Linf 1..8, sum bounds {SWEEP_SUM_BOUNDS}), COUNT+SUM+PRIVACY_ID_COUNT "
@@ -429,12 +460,15 @@ def main():
                                     f"{n:.2e} rows/GPU, {U:.1e} privacy ids, {P:.1e} Zipf({args.zipf}) partitions; "
                                     f"value = input rows/s for the whole analysis") if sweep else
                                    f"{args.workload}: DP {'COUNT+SUM' if count_sum else 'COUNT+SUM+MEAN'}, "
-                                   f"{n:.2e} rows/GPU, {U:.1e} privacy ids/GPU, {P:.1e} "
+                                   f"{n * world_size:.2e} rows on {world_size} GPU(s) ({n:.2e} rows/GPU), "
+                                   f"{U:.1e} privacy ids/GPU, {P:.1e} "
                                    f"{'public uniform' if public else f'Zipf({args.zipf})'} partitions, "
                                    f"L0={args.l0}, Linf={args.linf}, [0,10], Laplace, "
                                    f"{'no selection (public partitions)' if public else 'truncated-geometric selection'}"
                                    f", eps=1 delta=1e-6",
-                       "rows_per_gpu": n, "partitions": P, "privacy_ids_per_gpu": U,
+                       "rows_total": n * world_size, "rows_per_gpu": n, "partitions": P, "privacy_ids_per_gpu": U,
+                       **({"c4_node_shape": "4e9 rows / 5e7 partitions over 8 GPUs = 5e8 rows per GPU (this line: "
+                                            f"{world_size} GPU(s) x 5e8)"} if args.workload == "c4" else {}),
                        "parallelism": f"pid-sharded x{world_size}" + (" + RCCL reduce-scatter" if world else "")},
             "roofline": roofline,
             "roofline_e2e": {"definition": "rows/s x 24 B/row (int64 pid + int64 pk + f64 value read once) / "
@@ -448,10 +482,13 @@ def main():
                                                "never ships here); carried from BASELINE.md:28",
                                       "config": "COUNT+SUM+MEAN, 1e6 rows, 1e5 users, 17,770 Zipf(1.1) partitions, "
                                                 "L0=2, Linf=1"},
-            "fp64_sums": "per-partition fp64 sums use fp64 atomics: summation order, hence the last bits, vary run "
-                         "to run; counts and keep decisions are exact and deterministic",
+            "fp64_sums": "K4: per-partition sums accumulate in 64-bit fixed point (exact integer adds of each pair "
+                         "record's rint(x * 2^F), F = 62 - ceil(log2 max|x|)), so counts, sums and keep decisions are "
+                         "identical bit for bit run to run and for any grid (pdp_reduce.inc)",
             "kernels": stages, "rows_after_public_filter": rows_after_public_filter,
             "l0_prefilter_survivors": surv, **kept,
+            "k4_pair_slots": k4[0] if k4 else None, "k4_pairs": k4[1] if k4 else None,
+            "k4_passes": k4[2] if k4 else None,
             "kept_partitions_rank0": kept_parts,
             "sort_passes": int(st.sort_passes), "bucket_low_bits": int(st.bucket_low_bits),
             "fallback_rows": int(st.fallback_rows),

@@ -288,6 +288,11 @@ int pdp_generate_synthetic(int64_t* pid, int64_t* pk, double* value, int64_t n, 
                            int32_t value_kind, double value_lo, double value_hi, uint64_t seed,
                            void* stream);
 
+/* Device-to-device copy of `bytes` (a multiple of 16) with a 16-B-per-lane
+ * streaming kernel: bench.py's achievable-HBM ceiling (no reference
+ * counterpart; measurement only). */
+int pdp_stream_copy(const void* src, void* dst, int64_t bytes, void* stream);
+
 /* Statistics of the last pdp_bound_accumulate on this ctx (host values). */
 typedef struct pdp_stats {
   int64_t kept_rows_in;        /* rows after dropping non-public partitions */
@@ -298,6 +303,10 @@ typedef struct pdp_stats {
   int64_t sweep_cycles[4];     /* radix passes, debug stamps only: load, rank, look-back/bases, scatter */
   int64_t sweep_tiles;
   int64_t filter_rows;         /* rows that survived the L0 pre-filter (0: the filter did not run) */
+  int64_t k4_slots;            /* K4: pair slots written by K2 (+ generic-path groups); 0: K4 off */
+  int64_t k4_pairs;            /* K4: (pid, pk) pair records reduced */
+  int32_t k4_passes;           /* K4: radix passes on the partition block */
+  int32_t reserved_;
 } pdp_stats;
 int pdp_get_stats(pdp_ctx* ctx, pdp_stats* out);
 
@@ -316,7 +325,10 @@ enum {
   PDP_STAGE_ANALYSIS_METRICS = 9, /* utility analysis: per-configuration partition metrics + selection */
   PDP_STAGE_FILTER = 10,        /* K1f L0 pre-filter (one workgroup per privacy-id bucket) */
   PDP_STAGE_SURVIVOR_SORT = 11, /* radix sort of the pre-filter's survivors */
-  PDP_NUM_STAGES = 12,
+  PDP_STAGE_PAIR_PASS = 12,     /* K4 pair-record radix passes by partition block */
+  PDP_STAGE_REDUCE = 13,        /* K4 per-partition fixed-point reduction (+ shared-block zero / finalize) */
+  PDP_STAGE_ANALYSIS_SORT = 14, /* utility analysis: the (pk, pid) radix sort inside ANALYSIS_PAIRS */
+  PDP_NUM_STAGES = 15,
 };
 int pdp_profile_enable(pdp_ctx* ctx, int enable);
 /* Waits for recorded events; adds into ms_out/launches_out[PDP_NUM_STAGES]

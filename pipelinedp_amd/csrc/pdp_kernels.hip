@@ -66,7 +66,9 @@ enum Counter {
   kCtrAnaPairs = 13,  // utility analysis: pairs of sampled partitions
   kCtrNSurv = 14,     // rows that survive the L0 pre-filter (pdp_filter.inc)
   kCtrNDropped = 15,  // rows of non-public partitions seen by k_filter
-  kCtrTile0 = 16,  // 16..63 tile claim counters, one per onesweep launch
+  kCtrK4In = 16,      // K4: records in the first pair pass's input (slots + generic-path pairs)
+  kCtrK4Pairs = 17,   // K4: (pid, pk) pair records (non-empty slots)
+  kCtrTile0 = 18,  // 18..63 tile claim counters, one per onesweep launch
 };
 
 struct __align__(16) Rec {
@@ -111,7 +113,8 @@ __device__ __forceinline__ void st_rec(Rec* p, const Rec& r) {
 
 struct KeySpec {
   int mode;  // 0: key = pid >> low ; 1: key = (pid << pkb) | pk ; 3: key = (pid, bits(val)) 96-bit ;
-             // 4: bucketed pid: passes with shift >= 64 take the bucket digit (pid * mult) >> 32, others pid bits
+             // 4: bucketed pid: passes with shift >= 64 take the bucket digit (pid * mult) >> 32, others pid bits ;
+             // 6: K4 pair records {pk, count, x}: key = pk >> low (the partition block), empty slots dropped
   int passes;
   int shift[kMaxPasses];
   int bits[kMaxPasses];
@@ -143,6 +146,17 @@ struct SegParams {
   double smin, smax;
   int packed;  // row_count word holds (count << 32) | row_count until k_unpack_counts
   int debug;   // experiment flags (bench ablations), kDebugBatchKernel
+  // K4 (deterministic per-partition reduction, pdp_reduce.inc).  k4x != null: K2 writes one pair
+  // record {pk, count, x} per kept (pid, pk) group into slot k4x[s + i] of its segment [s, s + n)
+  // (empty records in the segment's other slots) instead of adding to the accumulators, and
+  // counts the records' partition-block digits in k4hist; VARIANCE writes {pk, 0, y} to k4y.
+  Rec* k4x;
+  Rec* k4y;
+  unsigned int* k4hist;  // [kK4Rep][kK4MaxPasses][256]
+  int k4sh;              // partition block = pk >> k4sh
+  int k4passes;
+  int k4shift[3];
+  int k4bits[3];
 };
 
 constexpr int kDebugBatchKernel = 4096;  // use k_segments even when k_lean applies
@@ -186,6 +200,9 @@ __device__ __forceinline__ uint32_t digit_of(const KeySpec& ks, int pass, const 
   const int sh = ks.shift[pass];
   uint64_t key;
   if (ks.mode == 0) {
+    key = (uint64_t)(r.pid >> ks.low);
+  } else if (ks.mode == 6) {
+    if (r.pid == 0xFFFFFFFFu) return 256u;  // empty slot
     key = (uint64_t)(r.pid >> ks.low);
   } else if (ks.mode == 4) {
     if (sh >= 64) return (uint32_t)(((uint64_t)r.pid * ks.mult) >> 32);
@@ -483,14 +500,17 @@ constexpr uint32_t kNoPos = 0xFFFFu;
 // its pid slot (k_filter rebuilds the pid), so no extra registers or LDS hold
 // it between the load and the scatter (a separate tag array spilled 64 B per
 // lane to scratch: ~8 GB of extra traffic per 1e9 rows).
+// rin2 / split (K4 pair passes): input record i is rin[i] for i < split, else rin2[i - split] (the
+// first pair pass reads K2's slots followed by the generic path's pairs).
 template <bool SOA, bool TAG = false>
-__global__ __launch_bounds__(kThreads, PDP_OS_OCC) void k_onesweep(
+__device__ __forceinline__ void onesweep_body(
     const int64_t* __restrict__ pid, const int64_t* __restrict__ pk, const double* __restrict__ val,
     const Rec* __restrict__ rin, Rec* __restrict__ rout, int64_t n_in,
     const unsigned long long* __restrict__ counters_n, int n_slot, KeySpec ks, int pass,
     const unsigned long long* __restrict__ off, unsigned long long* __restrict__ status, uint32_t epoch,
     unsigned long long* __restrict__ counters, int tile_slot, const unsigned int* __restrict__ tile_base,
-    uint32_t* __restrict__ tag_out, const uint32_t* __restrict__ tag_lo) {
+    uint32_t* __restrict__ tag_out, const uint32_t* __restrict__ tag_lo, const Rec* __restrict__ rin2,
+    int64_t split) {
   __shared__ Rec s_rec[kHalfTile];
   __shared__ uint32_t s_lo[TAG ? 256 : 1];
   __shared__ unsigned int s_cnt[4][kHist + 1];
@@ -551,7 +571,7 @@ __global__ __launch_bounds__(kThreads, PDP_OS_OCC) void k_onesweep(
             d = digit_of(ks, pass, r[k]);
         }
       } else {
-        r[k] = ld_rec(rin + idx);
+        r[k] = idx < split ? ld_rec(rin + idx) : ld_rec(rin2 + (idx - split));
         d = digit_of(ks, pass, r[k]);
       }
     }
@@ -573,7 +593,7 @@ __global__ __launch_bounds__(kThreads, PDP_OS_OCC) void k_onesweep(
   // bases are the sequential ones and the 16 atomics pipeline (no wave
   // barriers).  The base reaches the other peers by a lane shuffle.
   const uint64_t lt = (1ull << lane) - 1ull;
-  const bool any_invalid = SOA || tile_start + kTile > n_eff;
+  const bool any_invalid = SOA || ks.mode == 6 || tile_start + kTile > n_eff;
 #if PDP_OS_RANK_ATOMIC
   constexpr int kRankGroup = kItems < 8 ? kItems : 8;  // atomics in flight before their shuffles
 #pragma unroll
@@ -749,6 +769,36 @@ __global__ __launch_bounds__(kThreads, PDP_OS_OCC) void k_onesweep(
   (void)radix_bits;
 }
 
+// Distinct symbols per use, so rocprofv3 --stats (which truncates template
+// arguments with -T) reports each stage on its own line.
+#define PDP_ONESWEEP_ARGS                                                                                  \
+  const int64_t *__restrict__ pid, const int64_t *__restrict__ pk, const double *__restrict__ val,         \
+      const Rec *__restrict__ rin, Rec *__restrict__ rout, int64_t n_in,                                   \
+      const unsigned long long *__restrict__ counters_n, int n_slot, KeySpec ks, int pass,                 \
+      const unsigned long long *__restrict__ off, unsigned long long *__restrict__ status, uint32_t epoch, \
+      unsigned long long *__restrict__ counters, int tile_slot, const unsigned int *__restrict__ tile_base, \
+      uint32_t *__restrict__ tag_out, const uint32_t *__restrict__ tag_lo, const Rec *__restrict__ rin2,  \
+      int64_t split
+#define PDP_ONESWEEP_PASS                                                                                  \
+  pid, pk, val, rin, rout, n_in, counters_n, n_slot, ks, pass, off, status, epoch, counters, tile_slot,    \
+      tile_base, tag_out, tag_lo, rin2, split
+// records -> records (passes >= 1 of the pid sort, survivor sort, generic path)
+__global__ __launch_bounds__(kThreads, PDP_OS_OCC) void k_onesweep(PDP_ONESWEEP_ARGS) {
+  onesweep_body<false, false>(PDP_ONESWEEP_PASS);
+}
+// SoA columns -> records (first pass of the pid sort, non-public rows dropped)
+__global__ __launch_bounds__(kThreads, PDP_OS_OCC) void k_sort_first(PDP_ONESWEEP_ARGS) {
+  onesweep_body<true, false>(PDP_ONESWEEP_PASS);
+}
+// the L0 pre-filter's bucket pass (SoA columns -> tagged records + tags, pdp_filter.inc)
+__global__ __launch_bounds__(kThreads, PDP_OS_OCC) void k_bucket_pass(PDP_ONESWEEP_ARGS) {
+  onesweep_body<true, true>(PDP_ONESWEEP_PASS);
+}
+// K4 pair records by partition block (pdp_reduce.inc)
+__global__ __launch_bounds__(kThreads, PDP_OS_OCC) void k_pair_pass(PDP_ONESWEEP_ARGS) {
+  onesweep_body<false, false>(PDP_ONESWEEP_PASS);
+}
+
 // ---------------------------------------------------------------------------
 // K2: privacy-id buckets in LDS: bounding + per-(pid,pk) accumulation
 // ---------------------------------------------------------------------------
@@ -794,6 +844,7 @@ __device__ __forceinline__ void emit_group(const SegParams& sp, const AccPtrs& a
   if (sp.want_y) atomicAdd(&acc.y[pk], y);
 }
 
+#include "pdp_reduce.inc"
 #include "pdp_segments.inc"
 #include "pdp_thin.inc"
 #include "pdp_analysis.inc"
@@ -909,51 +960,58 @@ __global__ void k_stream_ranks(const Rec* __restrict__ sorted, int64_t m, const 
   }
 }
 
-__global__ void k_stream_rows(const Rec* __restrict__ r, int64_t m, const long long* __restrict__ gsc,
-                              const int32_t* __restrict__ grank, const uint8_t* __restrict__ row_keep, SegParams sp,
-                              unsigned long long* __restrict__ gcnt, double* __restrict__ gx,
-                              double* __restrict__ gy) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (int64_t)gridDim.x * blockDim.x) {
-    const long long g = gsc[i] - 1;
-    if (grank[g] >= sp.l0 || !row_keep[i]) continue;
-    double x, y;
-    row_terms(sp, r[i].val, x, y);
-    atomicAdd(&gcnt[g], 1ull);
-    if (sp.xmode != kXNone) atomicAdd(&gx[g], x);
-    if (sp.want_y) atomicAdd(&gy[g], y);
-  }
-}
-
+// Kept groups: the L_inf-kept rows of each L0-kept group summed in input
+// order (deterministic), then one accumulator add (or, K4, one pair record in
+// slot g of the generic path's pair array; sp.k4x / k4y point there).
 __global__ void k_stream_groups(const Rec* __restrict__ r, const long long* __restrict__ gpos,
-                                const int32_t* __restrict__ grank, int64_t ngroups, SegParams sp,
-                                const unsigned long long* __restrict__ gcnt, const double* __restrict__ gx,
-                                const double* __restrict__ gy, AccPtrs acc) {
+                                const int32_t* __restrict__ grank, const uint8_t* __restrict__ row_keep,
+                                int64_t ngroups, SegParams sp, AccPtrs acc) {
   for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < ngroups;
        g += (int64_t)gridDim.x * blockDim.x) {
-    if (grank[g] >= sp.l0 || gcnt[g] == 0) continue;
-    emit_group(sp, acc, r[gpos[g]].pk, (uint32_t)gcnt[g], gx[g], gy[g]);
+    uint32_t c = 0;
+    double x = 0.0, y = 0.0;
+    if (grank[g] < sp.l0) {
+      for (long long q = gpos[g]; q < gpos[g + 1]; ++q) {
+        if (!row_keep[q]) continue;
+        double xt, yt;
+        row_terms(sp, r[q].val, xt, yt);
+        ++c;
+        x += xt;
+        y += yt;
+      }
+    }
+    if (sp.k4x) {
+      if (c > 0) k4_put(sp, g, r[gpos[g]].pk, c, x, y, sp.k4hist);
+      else k4_empty(sp, g);
+    } else if (c > 0) {
+      emit_group(sp, acc, r[gpos[g]].pk, c, x, y);
+    }
   }
 }
 
 // contribution_bounds_already_enforced: every row is its own accumulator
 // (dp_engine.py:139-150, combiners.py create_accumulator([value])).
+// K4: row i -> slot i (empty for a dropped row).
 __global__ void k_enforced(const int64_t* __restrict__ pk, const double* __restrict__ val, int64_t n,
                            int64_t num_parts, SegParams sp, AccPtrs acc, unsigned long long* __restrict__ counters) {
+  k4_begin(sp);
   unsigned int invalid = 0;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t b = pk[i];
-    if (b < 0) continue;
-    if (b >= num_parts) {
-      ++invalid;
+    if (b < 0 || b >= num_parts) {
+      if (b >= num_parts) ++invalid;
+      if (sp.k4x) k4_empty(sp, i);
       continue;
     }
     double x = 0.0, y = 0.0;
     if (sp.has_value) {
       row_terms(sp, val[i], x, y);
     }
-    emit_group(sp, acc, (uint32_t)b, 1u, x, y);
+    if (sp.k4x) k4_put(sp, i, (uint32_t)b, 1u, x, y, k4_lds_hist());
+    else emit_group(sp, acc, (uint32_t)b, 1u, x, y);
   }
   if (invalid) atomicAdd(&counters[kCtrInvalid], (unsigned long long)invalid);
+  k4_end(sp);
 }
 
 // Packed (count << 32 | row_count) words -> the two int64 accumulators.
@@ -1163,6 +1221,26 @@ __global__ __launch_bounds__(kThreads) void k_shard_scatter(const int64_t* __res
 }
 
 // ---------------------------------------------------------------------------
+// Achievable-HBM probe (bench.py roofline.copy_peak_measured): 16 bytes per
+// lane, four loads in flight per lane before their stores -- the float4 copy
+// shape MI355X_MICROARCH.md measures at 6.29 TB/s.
+// ---------------------------------------------------------------------------
+
+__global__ __launch_bounds__(256) void k_stream_copy(const u32x4* __restrict__ src, u32x4* __restrict__ dst,
+                                                     int64_t n16) {
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  for (; i + 3 * stride < n16; i += 4 * stride) {
+    const u32x4 a = src[i], b = src[i + stride], c = src[i + 2 * stride], d = src[i + 3 * stride];
+    dst[i] = a;
+    dst[i + stride] = b;
+    dst[i + 2 * stride] = c;
+    dst[i + 3 * stride] = d;
+  }
+  for (; i < n16; i += stride) dst[i] = src[i];
+}
+
+// ---------------------------------------------------------------------------
 // Synthetic generator (oracle/pdp_oracle.py:synth_rows)
 // ---------------------------------------------------------------------------
 
@@ -1233,29 +1311,35 @@ int grid_for(int64_t n, int threads, int cap = 4096) {
 }
 
 struct Layout {
-  size_t recs_a, recs_b, recs_c, hist, off, counters, status, ranges, big, tags, tag_lo, keep, total;
+  size_t recs_a, recs_b, recs_c, hist, off, counters, status, ranges, big, tags, tag_lo, keep, k4rep, k4s, total;
   int64_t tiles;
   uint64_t big_cap;
 };
 
-Layout layout_for(int64_t n, bool sweep = false) {
+// k4p > 0: room for the K4 reduction over k4p partitions (pdp_reduce.inc): the
+// digit histogram replicas, the fixed-point scratch (lo, hi, flags per
+// partition), the look-back status of a pair pass over up to 2n records, and
+// with `variance` the y slots (in recs_c).
+Layout layout_for(int64_t n, bool sweep = false, int64_t k4p = 0, bool variance = false) {
   Layout L{};
   size_t o = 0;
   const size_t rb = align_up((size_t)std::max<int64_t>(n, 1) * sizeof(Rec), 256);
   L.recs_a = o; o += rb;
   L.recs_b = o; o += rb;
-  L.recs_c = o; o += sweep ? rb : 0;  // sweep: generic-path scratch that keeps the sorted rows intact
+  L.recs_c = o; o += (sweep || (k4p > 0 && variance)) ? rb : 0;  // sweep: generic-path scratch; K4: y slots
   L.hist = o; o += align_up(kMaxPasses * kHist * 8, 256);
   L.off = o; o += align_up(kMaxPasses * kHist * 8, 256);
   L.counters = o; o += align_up(kNumCounters * 8, 256);
   L.tiles = (std::max<int64_t>(n, 1) + kTile - 1) / kTile;
-  L.status = o; o += align_up((size_t)L.tiles * kStatusStride * 8, 256);
+  L.status = o; o += align_up((size_t)L.tiles * (k4p > 0 ? 2 : 1) * kStatusStride * 8, 256);
   L.ranges = o; o += align_up((size_t)kOverflowCap * 16, 256);
   L.big_cap = (uint64_t)std::max<int64_t>(n, 1) / 129 + 64;  // segments / batches of > 128 rows
   L.big = o; o += align_up((size_t)L.big_cap * 16, 256);
   L.tags = o; o += sweep ? 0 : align_up((size_t)std::max<int64_t>(n, 1) * 4, 256);  // L0 pre-filter tags
   L.tag_lo = o; o += 256 * 4;
   L.keep = o; o += sweep ? 0 : align_up((size_t)std::max<int64_t>(n, 1) / 4 + 64, 256);  // k_filter keep bytes
+  L.k4rep = o; o += k4p > 0 ? align_up((size_t)kK4Rep * kK4MaxPasses * 256 * 4, 256) : 0;
+  L.k4s = o; o += k4p > 0 ? align_up((size_t)k4p * 20, 256) : 0;
   L.total = o;
   return L;
 }
@@ -1315,7 +1399,7 @@ SegParams make_seg(const pdp_bound_params* bp, int low, int pkb, bool has_value)
 
 struct pdp_ctx {
   int device = 0;
-  unsigned int tile_slot = 16;  // next free onesweep tile-claim counter
+  unsigned int tile_slot = kCtrTile0;  // next free onesweep tile-claim counter
   bool prof = false;
   struct ProfRec {
     int stage;
@@ -1326,6 +1410,7 @@ struct pdp_ctx {
   double prof_ms[PDP_NUM_STAGES] = {};
   int64_t prof_n[PDP_NUM_STAGES] = {};
   void* last_ws = nullptr;
+  size_t status_ok = 0;  // bytes of the look-back status region cleared for the current epoch run
   uint32_t epoch = 0;
   pdp_stats stats{};
   std::vector<double> table_host;
@@ -1402,9 +1487,10 @@ struct ProfScope {
 };
 
 int next_epoch(pdp_ctx* ctx, hipStream_t stream, unsigned long long* status, size_t status_bytes, void* ws) {
-  if (ctx->last_ws != ws || ctx->epoch >= 0xFFFE) {
+  if (ctx->last_ws != ws || ctx->epoch >= 0xFFFE || status_bytes > ctx->status_ok) {
     HIP_TRY(hipMemsetAsync(status, 0, status_bytes, stream));
     ctx->last_ws = ws;
+    ctx->status_ok = status_bytes;
     ctx->epoch = 0;
   }
   ++ctx->epoch;
@@ -1493,10 +1579,11 @@ int sort_recs(pdp_ctx* ctx, Rec* a, Rec* b, int64_t m, const KeySpec& ks, unsign
       int rc = next_epoch(ctx, stream, status, status_bytes, ws);
       if (rc) return rc;
     }
-    hipLaunchKernelGGL((k_onesweep<false, false>), dim3((unsigned)tiles), dim3(kThreads), 0, stream,
+    hipLaunchKernelGGL(k_onesweep, dim3((unsigned)tiles), dim3(kThreads), 0, stream,
                        (const int64_t*)nullptr, (const int64_t*)nullptr, (const double*)nullptr, src, dst, m,
                        counters, (int)kCtrNGeneric, ks, p, off + p * kHist, status, ctx->epoch, counters,
-                       (int)ctx->tile_slot++, bases, (uint32_t*)nullptr, (const uint32_t*)nullptr);
+                       (int)ctx->tile_slot++, bases, (uint32_t*)nullptr, (const uint32_t*)nullptr,
+                       (const Rec*)nullptr, (int64_t)INT64_MAX);
     std::swap(src, dst);
   }
   HIP_TRY(hipGetLastError());
@@ -1533,11 +1620,16 @@ KeySpec composite_spec(int mode, int hi_bits, int lo_bits, int pkb, uint64_t U, 
 
 // `sorted` is only read (gather); `alt` is the generic sort's second buffer
 // (== sorted on the single-config path, a third buffer in a sweep so the
-// sorted rows survive for the next configuration).
+// sorted rows survive for the next configuration).  K4 (sp.k4x != null): the
+// slots buffer (`spare`) must not be touched, so the gather / sort buffers
+// are allocated here, and the kept groups' pair records go to an array of
+// one slot per group allocated in `keep` (*kf_x / *kf_y, *kf_n slots).
 int run_generic(pdp_ctx* ctx, const Rec* sorted, Rec* spare, Rec* alt, const std::vector<unsigned long long>& ranges,
-                const Plan& plan, const SegParams& sp, const pdp_bound_params* bp, uint64_t U, uint32_t P,
+                const Plan& plan, const SegParams& sp_in, const pdp_bound_params* bp, uint64_t U, uint32_t P,
                 AccPtrs acc, unsigned long long* hist, unsigned long long* off, unsigned long long* counters,
-                unsigned long long* status, size_t status_bytes, void* ws, hipStream_t stream) {
+                unsigned long long* status, size_t status_bytes, void* ws, hipStream_t stream, AsyncFrees* keep,
+                Rec** kf_x, Rec** kf_y, int64_t* kf_n) {
+  SegParams sp = sp_in;
   const int nr = (int)(ranges.size() / 2);
   std::vector<long long> rsrc(nr), rdst(nr);
   int64_t total = 0;
@@ -1548,8 +1640,13 @@ int run_generic(pdp_ctx* ctx, const Rec* sorted, Rec* spare, Rec* alt, const std
   }
   ctx->stats.fallback_rows = total;
   ctx->stats.fallback_ranges = nr;
+  if (kf_n) *kf_n = 0;
   if (total == 0) return 0;
   AsyncFrees scratch(stream);
+  if (sp.k4x) {
+    HIP_TRY(scratch.alloc((void**)&spare, (size_t)total * sizeof(Rec)));
+    HIP_TRY(scratch.alloc((void**)&alt, (size_t)total * sizeof(Rec)));
+  }
   long long *d_rsrc = nullptr, *d_rdst = nullptr;
   HIP_TRY(scratch.alloc((void**)&d_rsrc, nr * sizeof(long long)));
   HIP_TRY(scratch.alloc((void**)&d_rdst, nr * sizeof(long long)));
@@ -1608,19 +1705,17 @@ int run_generic(pdp_ctx* ctx, const Rec* sorted, Rec* spare, Rec* alt, const std
     return rc;
   hipLaunchKernelGGL(k_stream_ranks, dim3(ggr), dim3(kThreads), 0, stream, xs, (int64_t)ngroups, pfirst,
                      (int64_t)sp.l0, (uint8_t*)nullptr, grank);
-  // 4) accumulate kept rows per group, emit kept groups.
-  unsigned long long* gcnt;
-  double *gx, *gy;
-  HIP_TRY(scratch.alloc((void**)&gcnt, (size_t)ngroups * 8));
-  HIP_TRY(scratch.alloc((void**)&gx, (size_t)ngroups * 8));
-  HIP_TRY(scratch.alloc((void**)&gy, (size_t)ngroups * 8));
-  HIP_TRY(hipMemsetAsync(gcnt, 0, (size_t)ngroups * 8, stream));
-  HIP_TRY(hipMemsetAsync(gx, 0, (size_t)ngroups * 8, stream));
-  HIP_TRY(hipMemsetAsync(gy, 0, (size_t)ngroups * 8, stream));
-  hipLaunchKernelGGL(k_stream_rows, dim3(gr), dim3(kThreads), 0, stream, r, total, gsc, grank, row_keep, sp, gcnt,
-                     gx, gy);
-  hipLaunchKernelGGL(k_stream_groups, dim3(ggr), dim3(kThreads), 0, stream, r, gpos, grank, (int64_t)ngroups, sp,
-                     gcnt, gx, gy, acc);
+  // 4) kept groups: sums of the kept rows, then accumulators / pair records.
+  if (sp.k4x) {
+    HIP_TRY(keep->alloc((void**)&sp.k4x, (size_t)ngroups * sizeof(Rec)));
+    sp.k4y = nullptr;
+    if (sp.want_y) HIP_TRY(keep->alloc((void**)&sp.k4y, (size_t)ngroups * sizeof(Rec)));
+    *kf_x = sp.k4x;
+    *kf_y = sp.k4y;
+    *kf_n = ngroups;
+  }
+  hipLaunchKernelGGL(k_stream_groups, dim3(ggr), dim3(kThreads), 0, stream, r, gpos, grank, row_keep,
+                     (int64_t)ngroups, sp, acc);
   HIP_TRY(hipGetLastError());
   (void)r_other;
   return 0;
@@ -1679,6 +1774,8 @@ double noise_scale(int kind, double eps, double delta, double l0, double linf) {
   if (kind == PDP_NOISE_LAPLACE) return l0 * linf / eps;
   return pdp_gaussian_sigma(eps, delta, std::sqrt(l0) * linf);
 }
+
+bool k4_enabled(int64_t n, bool sweep);
 
 }  // namespace
 
@@ -1785,7 +1882,10 @@ int pdp_selection_threshold(int32_t selection, double eps, double delta, int64_t
 int pdp_workspace_size(const pdp_columns* cols, const pdp_bound_params* bp, size_t* bytes) {
   if (!cols || !bp || !bytes) return fail(PDP_ERR_INVALID_ARG, "null argument");
   if (cols->num_rows < 0) return fail(PDP_ERR_INVALID_ARG, "num_rows < 0");
-  *bytes = layout_for(cols->num_rows).total;
+  const bool k4 = k4_enabled(cols->num_rows, false);
+  *bytes = layout_for(cols->num_rows, false, k4 ? std::max<int64_t>(cols->num_partitions, 1) : 0,
+                      (bp->metrics & PDP_METRIC_VARIANCE) != 0)
+               .total;
   return 0;
 }
 
@@ -1841,6 +1941,132 @@ FilterPlan filter_plan(int64_t n, int64_t U, const pdp_bound_params* bp, int deb
   return f;
 }
 
+// K4 plan (pdp_reduce.inc): partition-block digits of the pair passes and the
+// fixed-point scales.  Off for the parameter sweep, for >= 2^32 rows (the
+// packed per-block counts) and with PDP_K4=0 (A/B experiments): the
+// accumulators then take fp64 atomics, as in round 2.
+struct K4Plan {
+  bool on;
+  int passes;
+  int shift[kK4MaxPasses], bits[kK4MaxPasses];
+  int fx, fy;  // fixed-point exponents: q = rint(x * 2^f)
+};
+
+// F = 62 - ceil(log2 M): |q| <= 2^62 for |x| <= M; sums of < 2^32 records stay exact in (lo, hi).
+int k4_exponent(double M) {
+  if (!(M > 0.0) || !std::isfinite(M)) return 0;
+  int e = 0;
+  (void)std::frexp(M, &e);  // M < 2^e
+  return std::max(-1000, std::min(1000, 62 - e));
+}
+
+bool k4_enabled(int64_t n, bool sweep) { return !sweep && n < (1ll << 32) && env_int("PDP_K4", 1) != 0; }
+
+K4Plan k4_plan(const pdp_bound_params* bp, const SegParams& sp, int64_t n, int64_t P, bool sweep) {
+  K4Plan k{};
+  k.on = k4_enabled(n, sweep);
+  if (!k.on) return k;
+  const int pkb = std::max(1, pdp::ceil_log2_u64((uint64_t)std::max<int64_t>(P, 1)));
+  const int kb = std::max(1, pkb - kK4Sh);
+  k.passes = (kb + 7) / 8;
+  int rem = kb, sh = 0;
+  for (int i = 0; i < k.passes; ++i) {
+    const int w = (rem + (k.passes - i) - 1) / (k.passes - i);
+    k.shift[i] = sh;
+    k.bits[i] = w;
+    sh += w;
+    rem -= w;
+  }
+  // largest |x| of one pair record: at most L_inf kept rows (one row when the bounds are already enforced)
+  const double linf = bp->bounds_already_enforced ? 1.0 : (double)bp->max_contributions_per_partition;
+  const double half = std::fabs(sp.b - sp.a) / 2.0;
+  double mx = 0.0;
+  if (sp.xmode == kXNsum) mx = linf * half;
+  else if (sp.xmode == kXClipSum) mx = linf * std::max(std::fabs(sp.a), std::fabs(sp.b));
+  else if (sp.xmode == kXRawSum) mx = std::max(std::fabs(sp.smin), std::fabs(sp.smax));
+  k.fx = k4_exponent(mx);
+  k.fy = k4_exponent(linf * half * half);
+  return k;
+}
+
+K4Red k4_red(const K4Plan& k, const SegParams& sp, int64_t P, bool y) {
+  K4Red r{};
+  const int f = y ? k.fy : k.fx;
+  r.sh = kK4Sh;
+  r.want_count = sp.want_count;
+  r.want_x = sp.xmode != kXNone;
+  r.P = P;
+  r.q = std::ldexp(1.0, f);
+  r.inv_hi = std::ldexp(1.0, 32 - f);
+  r.inv_lo = std::ldexp(1.0, -f);
+  return r;
+}
+
+// One K4 run: pair passes over [in_a (len_a) | in_b (len_b)] (ping-pong in
+// buf1 / buf2), then the chunked reduction into `acc` (y = the VARIANCE run).
+int k4_run(pdp_ctx* ctx, hipStream_t stream, const K4Plan& k, const K4Red& kr, bool y, const Rec* in_a,
+           int64_t len_a, const Rec* in_b, int64_t len_b, Rec* buf1, Rec* buf2, AccPtrs acc,
+           unsigned long long* off, unsigned long long* counters, unsigned long long* status, void* ws,
+           unsigned long long* s_lo, unsigned long long* s_hi, unsigned int* s_fl) {
+  const int64_t total = len_a + len_b;
+  if (total == 0) return 0;
+  hipLaunchKernelGGL(k4_set_counter, dim3(1), dim3(64), 0, stream, counters, (int)kCtrK4In,
+                     (unsigned long long)total);
+  KeySpec ks{};
+  ks.mode = 6;
+  ks.low = kr.sh;
+  ks.passes = k.passes;
+  for (int i = 0; i < k.passes; ++i) {
+    ks.shift[i] = k.shift[i];
+    ks.bits[i] = k.bits[i];
+  }
+  const int64_t tiles = (total + kTile - 1) / kTile;
+  const size_t status_bytes = (size_t)tiles * kStatusStride * 8;
+  const Rec* src = in_a;
+  Rec* dst = buf1;
+  {
+    ProfScope ps(ctx, PDP_STAGE_PAIR_PASS, stream);
+    for (int p = 0; p < k.passes; ++p) {
+      if (ctx->tile_slot >= kNumCounters) {
+        HIP_TRY(hipMemsetAsync(counters + kCtrTile0, 0, (kNumCounters - kCtrTile0) * 8, stream));
+        ctx->tile_slot = kCtrTile0;
+      }
+      if (int rc = next_epoch(ctx, stream, status, status_bytes, ws)) return rc;
+      hipLaunchKernelGGL(k_pair_pass, dim3((unsigned)tiles), dim3(kThreads), 0, stream, (const int64_t*)nullptr,
+                         (const int64_t*)nullptr, (const double*)nullptr, src, dst, (int64_t)0, counters,
+                         p == 0 ? (int)kCtrK4In : (int)kCtrK4Pairs, ks, p, off + p * kHist, status, ctx->epoch,
+                         counters, (int)ctx->tile_slot++, (const unsigned int*)nullptr, (uint32_t*)nullptr,
+                         (const uint32_t*)nullptr, p == 0 ? in_b : (const Rec*)nullptr,
+                         p == 0 ? len_a : (int64_t)INT64_MAX);
+      src = dst;
+      dst = (dst == buf1) ? buf2 : buf1;
+    }
+  }
+  HIP_TRY(hipGetLastError());
+  ProfScope ps(ctx, PDP_STAGE_REDUCE, stream);
+  const int64_t chunks = (total + kK4Chunk - 1) / kK4Chunk;
+  const bool scratch = (y || kr.want_x) && chunks > 1;
+  if (scratch)
+    hipLaunchKernelGGL(k4_zero_shared, dim3((unsigned)(chunks - 1)), dim3(kThreads), 0, stream, src, counters, kr.sh,
+                       kr.P, s_lo, s_hi, s_fl);
+  if (y)
+    hipLaunchKernelGGL(k4_reduce<true>, dim3((unsigned)chunks), dim3(kK4Threads), 0, stream, src, counters, kr, acc,
+                       s_lo, s_hi, s_fl);
+  else
+    hipLaunchKernelGGL(k4_reduce<false>, dim3((unsigned)chunks), dim3(kK4Threads), 0, stream, src, counters, kr, acc,
+                       s_lo, s_hi, s_fl);
+  if (scratch) {
+    if (y)
+      hipLaunchKernelGGL(k4_finalize<true>, dim3((unsigned)(chunks - 1)), dim3(kThreads), 0, stream, src, counters,
+                         kr, acc, s_lo, s_hi, s_fl);
+    else
+      hipLaunchKernelGGL(k4_finalize<false>, dim3((unsigned)(chunks - 1)), dim3(kThreads), 0, stream, src, counters,
+                         kr, acc, s_lo, s_hi, s_fl);
+  }
+  HIP_TRY(hipGetLastError());
+  return 0;
+}
+
 // pdp_bound_accumulate (nconf == 1, sweep == false) and
 // pdp_bound_accumulate_sweep: K0/K1 sort the rows by privacy id ONCE (the
 // order does not depend on L0 / L_inf / clipping), then K2 (+ KF) runs per
@@ -1892,7 +2118,8 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
   }
   if (n == 0) return 0;
 
-  const Layout L = layout_for(n, sweep);
+  const K4Plan k4 = k4_plan(bp, sp, n, P, sweep);
+  const Layout L = layout_for(n, sweep, k4.on ? P : 0, sp.want_y != 0);
   if (!workspace || workspace_bytes < L.total) return fail(PDP_ERR_WORKSPACE, "workspace too small");
   char* ws = (char*)workspace;
   Rec* recs_a = (Rec*)(ws + L.recs_a);
@@ -1905,14 +2132,54 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
   const size_t status_bytes = (size_t)L.tiles * kStatusStride * 8;
   HIP_TRY(hipMemsetAsync(ws + L.hist, 0, L.status - L.hist, stream));  // hist, off, counters
   ctx->tile_slot = kCtrTile0;
+  // K4 (pdp_reduce.inc): pair records into `slots` (+ the y slots), then pair passes + reduction
+  unsigned int* k4rep = (unsigned int*)(ws + L.k4rep);
+  unsigned long long* k4lo = (unsigned long long*)(ws + L.k4s);
+  unsigned long long* k4hi = k4lo + P;
+  unsigned int* k4fl = (unsigned int*)(k4hi + P);
+  Rec* k4y = sp.want_y ? (Rec*)(ws + L.recs_c) : nullptr;
+  auto k4_attach = [&](SegParams& q, Rec* slots) {
+    if (!k4.on) return;
+    q.packed = 0;
+    q.k4x = slots;
+    q.k4y = k4y;
+    q.k4hist = k4rep;
+    q.k4sh = kK4Sh;
+    q.k4passes = k4.passes;
+    for (int i = 0; i < kK4MaxPasses; ++i) {
+      q.k4shift[i] = k4.shift[i];
+      q.k4bits[i] = k4.bits[i];
+    }
+  };
+  // after K2 (+ KF): x run over [slots | generic-path pairs], then the y run (VARIANCE)
+  auto k4_finish = [&](const SegParams& q, const Rec* slots, int64_t nslots, const Rec* kfx, const Rec* kfy,
+                       int64_t nkf, Rec* buf1, Rec* buf2) -> int {
+    hipLaunchKernelGGL(k4_offsets, dim3(1), dim3(kThreads), 0, stream, k4rep, k4.passes, off, counters);
+    ctx->stats.k4_slots = nslots + nkf;
+    ctx->stats.k4_passes = k4.passes;
+    if (int rc = k4_run(ctx, stream, k4, k4_red(k4, q, P, false), false, slots, nslots, kfx, nkf, buf1, buf2, acc, off,
+                        counters, status, workspace, k4lo, k4hi, k4fl))
+      return rc;
+    if (q.want_y) {
+      if (int rc = k4_run(ctx, stream, k4, k4_red(k4, q, P, true), true, k4y, nslots, kfy, nkf, buf1, buf2, acc, off,
+                          counters, status, workspace, k4lo, k4hi, k4fl))
+        return rc;
+    }
+    return 0;
+  };
+  if (k4.on) HIP_TRY(hipMemsetAsync(k4rep, 0, (size_t)kK4Rep * kK4MaxPasses * 256 * 4, stream));
 
   if (bp->bounds_already_enforced) {
+    k4_attach(sp, recs_a);
     {
       ProfScope ps(ctx, PDP_STAGE_ENFORCED, stream);
       hipLaunchKernelGGL(k_enforced, dim3(grid_for(n, kThreads, 8192)), dim3(kThreads), 0, stream, cols->pk,
                        cols->value, n, P, sp, acc, counters);
     }
     HIP_TRY(hipGetLastError());
+    if (k4.on) {
+      if (int rc = k4_finish(sp, recs_a, n, nullptr, nullptr, 0, recs_b, recs_a)) return rc;
+    }
     unsigned long long inv = 0;
     HIP_TRY(hipMemcpyAsync(&inv, counters + kCtrInvalid, 8, hipMemcpyDeviceToHost, stream));
     HIP_TRY(hipStreamSynchronize(stream));
@@ -1920,7 +2187,7 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
     return 0;
   }
 
-  sp.packed = sp.want_count && n < (1ll << 32);
+  sp.packed = !k4.on && sp.want_count && n < (1ll << 32);
   KeySpec ks{};
   ks.mode = 0;
   ks.low = plan.low;
@@ -1982,19 +2249,21 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
     }
     ProfScope ps(ctx, p == 0 ? PDP_STAGE_ONESWEEP_FIRST : PDP_STAGE_ONESWEEP_REST, stream);
     if (p == 0 && fpl.on)
-      hipLaunchKernelGGL((k_onesweep<true, true>), dim3((unsigned)L.tiles), dim3(kThreads), 0, stream, cols->pid,
+      hipLaunchKernelGGL(k_bucket_pass, dim3((unsigned)L.tiles), dim3(kThreads), 0, stream, cols->pid,
                          cols->pk, cols->value, (const Rec*)nullptr, dst, n, counters, (int)kCtrNKept, ks, p,
-                         off + p * kHist, status, ctx->epoch, counters, (int)ctx->tile_slot++, bases, tags, tag_lo);
+                         off + p * kHist, status, ctx->epoch, counters, (int)ctx->tile_slot++, bases, tags, tag_lo,
+                         (const Rec*)nullptr, (int64_t)INT64_MAX);
     else if (p == 0)
-      hipLaunchKernelGGL((k_onesweep<true, false>), dim3((unsigned)L.tiles), dim3(kThreads), 0, stream, cols->pid,
+      hipLaunchKernelGGL(k_sort_first, dim3((unsigned)L.tiles), dim3(kThreads), 0, stream, cols->pid,
                          cols->pk, cols->value, (const Rec*)nullptr, dst, n, counters, (int)kCtrNKept, ks, p,
                          off + p * kHist, status, ctx->epoch, counters, (int)ctx->tile_slot++, bases,
-                         (uint32_t*)nullptr, (const uint32_t*)nullptr);
+                         (uint32_t*)nullptr, (const uint32_t*)nullptr, (const Rec*)nullptr, (int64_t)INT64_MAX);
     else
-      hipLaunchKernelGGL((k_onesweep<false, false>), dim3((unsigned)L.tiles), dim3(kThreads), 0, stream,
+      hipLaunchKernelGGL(k_onesweep, dim3((unsigned)L.tiles), dim3(kThreads), 0, stream,
                          (const int64_t*)nullptr, (const int64_t*)nullptr, (const double*)nullptr, src, dst, n,
                          counters, (int)kCtrNKept, ks, p, off + p * kHist, status, ctx->epoch, counters,
-                         (int)ctx->tile_slot++, bases, (uint32_t*)nullptr, (const uint32_t*)nullptr);
+                         (int)ctx->tile_slot++, bases, (uint32_t*)nullptr, (const uint32_t*)nullptr,
+                         (const Rec*)nullptr, (int64_t)INT64_MAX);
     src = dst;
     dst = (dst == recs_a) ? recs_b : recs_a;
   }
@@ -2058,7 +2327,8 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
   bp = &bps[c];
   sp = sps[c];
   acc = accs[c];
-  sp.packed = sp.want_count && n < (1ll << 32);
+  sp.packed = !k4.on && sp.want_count && n < (1ll << 32);
+  k4_attach(sp, spare);
   if (c > 0) {
     // fresh K2/KF counters; the kept-row count of the shared sort stays
     unsigned long long reset[kCtrSweepCycles] = {};
@@ -2073,8 +2343,9 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
                       !(sp.debug & (kDebugBatchKernel | kDebugNoThin));
     if (thin) {
       const int64_t waves = ((int64_t)n_sorted + kThinChunk - 1) / kThinChunk;
-      // LDS partition cache on: the Zipf-head pairs' HBM atomics otherwise dominate (c3: K2 8.1 -> 3.4 ms)
-      const bool tcache = env_int("PDP_THIN_CACHE", 1) != 0;
+      // LDS partition cache on: the Zipf-head pairs' HBM atomics otherwise dominate (c3: K2 8.1 -> 3.4 ms);
+      // K4 writes pair records instead of atomics, no cache
+      const bool tcache = !k4.on && env_int("PDP_THIN_CACHE", 1) != 0;
       const int64_t blocks =
           std::max<int64_t>(1, std::min<int64_t>((waves + 3) / 4, env_int("PDP_THIN_BLOCKS", 8192)));
       const int64_t l0 = bp->max_partitions_contributed;
@@ -2092,7 +2363,8 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
       const bool sorted_l0 = bp->max_partitions_contributed >= kSortMinL0 && !(sp.debug & kDebugLeanMinSearch);
       // the LDS partition cache pays when many privacy ids keep the same hot partitions, which grows with
       // L0: c4 (L0 = 32) K2 137 -> 50 ms (round 1); at c3 (L0 = 4) / c2 (L0 = 8) it does not pay
-      const bool cache = (bp->max_partitions_contributed >= kHotMinL0 || (sp.debug & kDebugForceHotCache) ||
+      const bool cache = !k4.on &&
+                         (bp->max_partitions_contributed >= kHotMinL0 || (sp.debug & kDebugForceHotCache) ||
                           (fpl.on && env_int("PDP_K2_CACHE", 0))) &&
                          !(sp.debug & kDebugNoHotCache);
       const bool two = bp->max_partitions_contributed > 64;
@@ -2120,28 +2392,51 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
   if (host_ctr[kCtrErr]) return fail(PDP_ERR_INTERNAL, "radix look-back timed out");
   if (host_ctr[kCtrInvalid]) return fail(PDP_ERR_OUT_OF_RANGE, "privacy id or partition id out of range");
   std::vector<unsigned long long> rg;
+  int64_t k4_slots = (int64_t)host_ctr[n_slot];  // K2's slots (K4)
   if (host_ctr[kCtrFull]) {
     // Too many overflowing buckets: redo everything on the generic path.
-    HIP_TRY(hipMemsetAsync(acc.row_count, 0, (size_t)P * 8, stream));
-    if (acc.count) HIP_TRY(hipMemsetAsync(acc.count, 0, (size_t)P * 8, stream));
-    if (acc.x) HIP_TRY(hipMemsetAsync(acc.x, 0, (size_t)P * 8, stream));
-    if (acc.y) HIP_TRY(hipMemsetAsync(acc.y, 0, (size_t)P * 8, stream));
+    if (k4.on) {
+      HIP_TRY(hipMemsetAsync(k4rep, 0, (size_t)kK4Rep * kK4MaxPasses * 256 * 4, stream));  // drop K2's records
+      k4_slots = 0;
+    } else {
+      HIP_TRY(hipMemsetAsync(acc.row_count, 0, (size_t)P * 8, stream));
+      if (acc.count) HIP_TRY(hipMemsetAsync(acc.count, 0, (size_t)P * 8, stream));
+      if (acc.x) HIP_TRY(hipMemsetAsync(acc.x, 0, (size_t)P * 8, stream));
+      if (acc.y) HIP_TRY(hipMemsetAsync(acc.y, 0, (size_t)P * 8, stream));
+    }
     rg = {0ull, host_ctr[n_slot]};
   } else if (host_ctr[kCtrNRanges]) {
     rg.resize(2 * host_ctr[kCtrNRanges]);
     HIP_TRY(hipMemcpyAsync(rg.data(), ranges, rg.size() * 8, hipMemcpyDeviceToHost, stream));
     HIP_TRY(hipStreamSynchronize(stream));
+    if (k4.on) {  // the generic path's pairs come in their own array: empty these slots
+      const int nr = (int)host_ctr[kCtrNRanges];
+      hipLaunchKernelGGL(k4_fill_ranges, dim3((unsigned)std::min(nr, 4096)), dim3(kThreads), 0, stream, sp, ranges,
+                         nr);
+    }
   }
+  AsyncFrees k4keep(stream);  // the generic path's pair arrays (until the K4 runs are enqueued)
+  Rec *kfx = nullptr, *kfy = nullptr;
+  int64_t nkf = 0;
   if (!rg.empty()) {
-    int rc = run_generic(ctx, sorted, spare, alt, rg, plan, sp, bp, ks.num_pids, ks.num_parts, acc, hist, off,
-                         counters, status, status_bytes, workspace, stream);
+    SegParams gsp = sp;
+    if (k4.on) gsp.k4hist = k4rep;  // replica 0: global atomics from the generic path
+    int rc = run_generic(ctx, sorted, spare, alt, rg, plan, gsp, bp, ks.num_pids, ks.num_parts, acc, hist, off,
+                         counters, status, status_bytes, workspace, stream, &k4keep, &kfx, &kfy, &nkf);
     if (rc) return rc;
     unsigned long long err = 0;
     HIP_TRY(hipMemcpyAsync(&err, counters + kCtrErr, 8, hipMemcpyDeviceToHost, stream));
     HIP_TRY(hipStreamSynchronize(stream));
     if (err) return fail(PDP_ERR_INTERNAL, "radix look-back timed out (generic path)");
   }
-  if (sp.packed) {
+  if (k4.on) {
+    if (int rc = k4_finish(sp, spare, k4_slots, kfx, kfy, nkf, sorted, spare)) return rc;
+    unsigned long long kc[kCtrK4Pairs + 1];
+    HIP_TRY(hipMemcpyAsync(kc, counters, sizeof(kc), hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipStreamSynchronize(stream));
+    ctx->stats.k4_pairs = (int64_t)kc[kCtrK4Pairs];
+    if (kc[kCtrErr]) return fail(PDP_ERR_INTERNAL, "radix look-back timed out (pair passes)");
+  } else if (sp.packed) {
     hipLaunchKernelGGL(k_unpack_counts, dim3(grid_for(P, kThreads, 4096)), dim3(kThreads), 0, stream, acc.row_count,
                        acc.count, P);
     HIP_TRY(hipGetLastError());
@@ -2312,7 +2607,8 @@ int analysis_impl(pdp_ctx* ctx, const int64_t* pid, const int64_t* pk, const dou
       const int pidbits = std::max(1, pdp::ceil_log2_u64((uint64_t)U + 1));
       KeySpec ks = composite_spec(1, pkbits, pidbits, pidbits, (uint32_t)std::min<int64_t>(U, 0xFFFFFFFFll),
                                   (uint32_t)P);
-      if (int rc = sort_recs(ctx, ra, rb, n, ks, hist, off, counters, status, status_bytes, workspace, stream, &sorted))
+      if (int rc = sort_recs(ctx, ra, rb, n, ks, hist, off, counters, status, status_bytes, workspace, stream, &sorted,
+                             PDP_STAGE_ANALYSIS_SORT))
         return rc;
       hipLaunchKernelGGL(k_ana_group_flags, dim3(g), dim3(kThreads), 0, stream, sorted, n, flags);
       if (int rc = scan_inplace(flags, n, stream)) return rc;
@@ -2331,7 +2627,8 @@ int analysis_impl(pdp_ctx* ctx, const int64_t* pid, const int64_t* pk, const dou
         ks.bits[ks.passes] = std::min(8, pkbits - sh);
         ++ks.passes;
       }
-      if (int rc = sort_recs(ctx, ra, rb, n, ks, hist, off, counters, status, status_bytes, workspace, stream, &sorted))
+      if (int rc = sort_recs(ctx, ra, rb, n, ks, hist, off, counters, status, status_bytes, workspace, stream, &sorted,
+                             PDP_STAGE_ANALYSIS_SORT))
         return rc;
       hipLaunchKernelGGL(k_ana_pairs_pre, dim3(g), dim3(kThreads), 0, stream, sorted, n, pre_count, pre_npart, ppk,
                          pref, pcnt, psum, npart);
@@ -2650,6 +2947,15 @@ int pdp_generate_synthetic(int64_t* pid, int64_t* pk, double* value, int64_t n, 
   if (n == 0) return 0;
   hipLaunchKernelGGL(k_generate, dim3(grid_for(n, kThreads, 16384)), dim3(kThreads), 0, (hipStream_t)stream, pid, pk,
                      value, n, row_offset, U, P, zipf_s, value_kind, lo, hi, seed);
+  HIP_TRY(hipGetLastError());
+  return 0;
+}
+
+int pdp_stream_copy(const void* src, void* dst, int64_t bytes, void* stream) {
+  if (bytes < 0 || (bytes & 15) || (bytes && (!src || !dst))) return fail(PDP_ERR_INVALID_ARG, "bad copy args");
+  if (bytes == 0) return 0;
+  hipLaunchKernelGGL(k_stream_copy, dim3(8192), dim3(256), 0, (hipStream_t)stream, (const u32x4*)src, (u32x4*)dst,
+                     bytes / 16);
   HIP_TRY(hipGetLastError());
   return 0;
 }

@@ -180,13 +180,17 @@ class DPResult:
                                  enforced, backend.sampling_seed, backend._debug_force_fallback)
         rel = self._release_config(mask)  # raises before any work if budgets are not computed
         need_value = bool(mask & (native.METRIC_SUM | native.METRIC_MEAN | native.METRIC_VARIANCE))
-        world = backend.world if backend.world is not None and backend.world.size > 1 else None
+        # A World (also of size 1: the RCCL identity, tests/test_gpu_rccl.py) runs the collective path.
+        world = backend.world
         pid, pk, value, U, P, keys = self._inputs(torch, ex.device, not enforced, need_value, world)
         fields = native.metric_fields(mask)
+        if world is not None and world.size > 1:
+            # every rank must take the same branch below (a rank with P == 0 alone would leave the others
+            # blocked in the collectives): agree on P first, raising on disagreement
+            world.check_same(P, "num_partitions", pk.device)
         if P == 0:  # e.g. public_partitions=[]: nothing to release (reference: empty collection)
             return keys, np.zeros(0, dtype=bool), fields, np.zeros((len(fields), 0))
         if world is not None:
-            world.check_same(P, "num_partitions", pk.device)
             presharded = isinstance(self._col, ColumnarData) and self._col.privacy_id_sharded
             keep, out, fields = world.aggregate(ex, pid, pk, value, U, P, bounds, rel, shuffle=not presharded)
         else:

@@ -67,7 +67,8 @@ class AnalysisOutputs(ctypes.Structure):
 class Stats(ctypes.Structure):
     _fields_ = [("kept_rows_in", c_i64), ("fallback_rows", c_i64), ("fallback_ranges", c_i64),
                 ("sort_passes", c_i32), ("bucket_low_bits", c_i32), ("sweep_cycles", c_i64 * 4),
-                ("sweep_tiles", c_i64), ("filter_rows", c_i64)]
+                ("sweep_tiles", c_i64), ("filter_rows", c_i64), ("k4_slots", c_i64), ("k4_pairs", c_i64),
+                ("k4_passes", c_i32), ("reserved_", c_i32)]
 
 
 # Every symbol declared in include/pdp_hip.h: (name, restype, argtypes).
@@ -105,13 +106,15 @@ SIGNATURES = [
                                ctypes.c_size_t, c_vp]),
     ("pdp_generate_synthetic", c_i32, [c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_f64, c_i32, c_f64,
                                        c_f64, c_u64, c_vp]),
+    ("pdp_stream_copy", c_i32, [c_vp, c_vp, c_i64, c_vp]),
     ("pdp_get_stats", c_i32, [c_vp, ctypes.POINTER(Stats)]),
     ("pdp_profile_enable", c_i32, [c_vp, c_i32]),
     ("pdp_profile_read", c_i32, [c_vp, ctypes.POINTER(c_f64), ctypes.POINTER(c_i64), c_i32]),
 ]
 
 STAGES = ["histogram", "onesweep_first", "onesweep_rest", "buckets", "generic", "release", "enforced",
-          "tile_counts", "analysis_pairs", "analysis_metrics", "filter", "survivor_sort"]
+          "tile_counts", "analysis_pairs", "analysis_metrics", "filter", "survivor_sort", "pair_pass", "reduce",
+          "analysis_sort"]
 
 _lib = None
 

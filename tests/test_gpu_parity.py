@@ -229,15 +229,72 @@ def test_already_enforced_matches_oracle(ex):
     check_acc(ref, rc, cnt, x, None, 1 | 2, val)
 
 
-def test_determinism_of_counts(ex):
+def _with_env(name, value, fn):
+    import os
+    old = os.environ.get(name)
+    os.environ[name] = value
+    try:
+        return fn()
+    finally:
+        if old is None:
+            del os.environ[name]
+        else:
+            os.environ[name] = old
+
+
+@pytest.mark.parametrize("flags", [0, FORCE_FILTER, NO_THIN | FORCE_FILTER, BATCH_KERNEL])
+def test_determinism_of_counts_and_sums(ex, flags):
+    """K4 (pdp_reduce.inc): counts AND fp64 sums are identical bit for bit run
+    to run and whatever the K2 grid (the records reach the fixed-point
+    accumulators in a different order), for every K2 kernel."""
     n, U, P = 200000, 5000, 2000
     pid, pk, val = o.synth_rows(n, U, P, seed=21, zipf_s=1.1)
     bp = o.BoundParams(4, 2, 0.0, 10.0)
-    r1 = run_gpu(ex, pid, pk, val, U, P, bp, 1 | 4, seed=5)
-    r2 = run_gpu(ex, pid, pk, val, U, P, bp, 1 | 4, seed=5)
-    np.testing.assert_array_equal(r1[2], r2[2])
-    np.testing.assert_array_equal(r1[3], r2[3])
-    np.testing.assert_allclose(r1[4], r2[4], rtol=1e-12, atol=1e-9)
+    mask = 1 | 4 | 8 | 16
+    r1 = run_gpu(ex, pid, pk, val, U, P, bp, mask, seed=5, debug_flags=flags)
+    r2 = run_gpu(ex, pid, pk, val, U, P, bp, mask, seed=5, debug_flags=flags)
+    r3 = _with_env("PDP_THIN_BLOCKS", "7", lambda: _with_env(
+        "PDP_K2_BLOCKS", "5", lambda: run_gpu(ex, pid, pk, val, U, P, bp, mask, seed=5, debug_flags=flags)))
+    for r in (r2, r3):
+        for i in (2, 3, 4, 5):
+            np.testing.assert_array_equal(r1[i], r[i])
+    ref = o.bound_and_accumulate(pid, pk, val, P, bp, "hash", seed=5)
+    check_acc(ref, r1[2], r1[3], r1[4], r1[5], mask, val)
+
+
+@pytest.mark.parametrize("cfgi", [0, 2, 3, 5, 9, 11, 16, 20])
+def test_k4_reduction_matches_atomic_path(ex, cfgi):
+    """The K4 pair-record reduction against the round-2 fp64-atomic
+    accumulation (PDP_K4=0) on the same bounding: counts bit-exact, sums to
+    1e-12 relative (only the summation differs)."""
+    n, U, P, z, L0, Linf, vb, pb, mask = CONFIGS[cfgi]
+    pid, pk, val = o.synth_rows(n, U, P, seed=100 + cfgi, zipf_s=z, value_lo=-5, value_hi=15)
+    bp = o.BoundParams(L0, Linf, *(vb or (None, None)), *(pb or (None, None)))
+    a = run_gpu(ex, pid, pk, val, U, P, bp, mask, seed=7)
+    b = _with_env("PDP_K4", "0", lambda: run_gpu(ex, pid, pk, val, U, P, bp, mask, seed=7))
+    np.testing.assert_array_equal(a[2], b[2])
+    if a[3] is not None:
+        np.testing.assert_array_equal(a[3], b[3])
+    for i in (4, 5):
+        if a[i] is not None:
+            np.testing.assert_allclose(a[i], b[i], rtol=1e-12, atol=1e-9)
+
+
+def test_nan_values_propagate_to_their_partition(ex):
+    """A NaN value reaches its partition's sum as NaN (np.clip / sum
+    semantics of combiners.py:254-261, 305-311); other partitions are
+    unaffected."""
+    n, U, P = 20000, 400, 300
+    pid, pk, val = o.synth_rows(n, U, P, seed=19)
+    val = val.copy()
+    bad = np.flatnonzero(pk == 7)
+    val[bad] = np.nan
+    bp = o.BoundParams(400, 400, 0.0, 10.0)  # non-binding: every row kept
+    _, _, rc, cnt, x, _ = run_gpu(ex, pid, pk, val, U, P, bp, 1 | 2, seed=3)
+    assert np.isnan(x[7])
+    ok = np.arange(P) != 7
+    np.testing.assert_allclose(x[ok], np.bincount(pk, np.clip(np.nan_to_num(val), 0, 10), P)[ok], rtol=1e-12)
+    np.testing.assert_array_equal(cnt, np.bincount(pk, minlength=P))
 
 
 # ---------------------------------------------------------------------------

@@ -1,10 +1,12 @@
-"""The multi-GPU path (World.aggregate: rank-local bound+accumulate, RCCL
-reduce-scatter of the [P] accumulators, owner-side release) on the nccl
-(= RCCL) backend with real device tensors.  One GPU box => world size 1, so
-this checks the collective calls (dtypes, shapes, layouts) on RCCL; the
+"""The multi-GPU path (World.aggregate: [privacy-id shuffle by all-to-all,]
+rank-local bound+accumulate, RCCL reduce-scatter of the [P] accumulators,
+owner-side release, all-gather) on the nccl (= RCCL) backend with real
+device tensors and the HIP library.  One GPU box => world size 1, so these
+check the collective calls (dtypes, shapes, layouts, splits) on RCCL; the
 world-size-2 data flow is covered by the gloo tests (tests/test_distributed.py).
-Must equal the single-process path bit-exactly: the reduce-scatter of one rank
-is the identity and Philox noise is keyed by the global partition id."""
+Must equal the single-process path bit-exactly: the shuffle and the
+reduce-scatter of one rank are the identity, K4 sums are exact, and Philox
+noise is keyed by the global partition id."""
 import socket
 
 import numpy as np
@@ -21,37 +23,89 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def test_world_aggregate_on_rccl_matches_single_process():
+@pytest.fixture(scope="module")
+def rccl():
     import torch
     import torch.distributed as dist
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0, world_size=1,
+                            device_id=torch.device("cuda", 0))
+    yield
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("shuffle", [False, True])
+def test_world_aggregate_on_rccl_matches_single_process(rccl, shuffle):
+    import torch
     from pipelinedp_amd import native
     from pipelinedp_amd.distributed import World
     from pipelinedp_amd.executor import BoundConfig, HipExecutor, ReleaseConfig
 
-    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0, world_size=1,
-                            device_id=torch.device("cuda", 0))
-    try:
-        ex = HipExecutor(0)
-        n, U, P = 50000, 900, 777
-        pid, pk, val = o.synth_rows(n, U, P, seed=21, zipf_s=1.1)
-        d = lambda a: torch.from_numpy(a).cuda()  # noqa: E731
-        mask = native.METRIC_COUNT | native.METRIC_SUM | native.METRIC_MEAN | native.METRIC_PRIVACY_ID_COUNT
-        bounds = BoundConfig(mask, 3, 2, 0.0, 10.0, sampling_seed=5)
-        eps = [0.0] * native.NUM_MECH
-        delta = [0.0] * native.NUM_MECH
-        eps[native.MECH_MEAN], eps[native.MECH_PRIVACY_ID_COUNT] = 0.4, 0.3
-        eps[native.MECH_SELECTION], delta[native.MECH_SELECTION] = 0.3, 1e-5
-        rel = ReleaseConfig(mask, native.NOISE_LAPLACE, native.SELECTION_TRUNCATED_GEOMETRIC, eps, delta,
-                            noise_seed=9)
-        world = World(0, 1)
-        k1, m1, f1 = world.aggregate(ex, d(pid), d(pk), d(val), U, P, bounds, rel, gather=True)
-        acc = ex.accumulate(d(pid), d(pk), d(val), U, P, bounds)
-        k2, m2, f2 = ex.release(acc, rel, bounds)
-        torch.cuda.synchronize()
-        assert f1 == f2
-        np.testing.assert_array_equal(k1.cpu().numpy(), k2[:P].cpu().numpy())
-        kept = k2[:P].bool().cpu().numpy()
-        a, b = m1.cpu().numpy()[:, kept], m2[:, :P].cpu().numpy()[:, kept]
-        np.testing.assert_allclose(a, b, rtol=1e-9, atol=1e-9)
-    finally:
-        dist.destroy_process_group()
+    ex = HipExecutor(0)
+    n, U, P = 50000, 900, 777
+    pid, pk, val = o.synth_rows(n, U, P, seed=21, zipf_s=1.1)
+    d = lambda a: torch.from_numpy(a).cuda()  # noqa: E731
+    mask = native.METRIC_COUNT | native.METRIC_SUM | native.METRIC_MEAN | native.METRIC_PRIVACY_ID_COUNT
+    bounds = BoundConfig(mask, 3, 2, 0.0, 10.0, sampling_seed=5)
+    eps = [0.0] * native.NUM_MECH
+    delta = [0.0] * native.NUM_MECH
+    eps[native.MECH_MEAN], eps[native.MECH_PRIVACY_ID_COUNT] = 0.4, 0.3
+    eps[native.MECH_SELECTION], delta[native.MECH_SELECTION] = 0.3, 1e-5
+    rel = ReleaseConfig(mask, native.NOISE_LAPLACE, native.SELECTION_TRUNCATED_GEOMETRIC, eps, delta,
+                        noise_seed=9)
+    world = World(0, 1)
+    k1, m1, f1 = world.aggregate(ex, d(pid), d(pk), d(val), U, P, bounds, rel, gather=True, shuffle=shuffle)
+    acc = ex.accumulate(d(pid), d(pk), d(val), U, P, bounds)
+    k2, m2, f2 = ex.release(acc, rel, bounds)
+    torch.cuda.synchronize()
+    assert f1 == f2
+    np.testing.assert_array_equal(k1.cpu().numpy(), k2[:P].cpu().numpy())
+    kept = k2[:P].bool().cpu().numpy()
+    a, b = m1.cpu().numpy()[:, kept], m2[:, :P].cpu().numpy()[:, kept]
+    np.testing.assert_array_equal(a, b)
+
+
+def test_shuffle_by_privacy_id_on_rccl_keeps_rows(rccl):
+    """World.shuffle_by_privacy_id at world size 1: pdp_shard_rows + the
+    all_to_all_single calls return every row, in input order."""
+    import torch
+    from pipelinedp_amd.distributed import World
+    from pipelinedp_amd.executor import HipExecutor
+    ex = HipExecutor(0)
+    pid, pk, val = o.synth_rows(20000, 700, 300, seed=3)
+    d = lambda a: torch.from_numpy(a).cuda()  # noqa: E731
+    a, b, c = World(0, 1).shuffle_by_privacy_id(ex, d(pid), d(pk), d(val))
+    np.testing.assert_array_equal(a.cpu().numpy(), pid)
+    np.testing.assert_array_equal(b.cpu().numpy(), pk)
+    np.testing.assert_array_equal(c.cpu().numpy(), val)
+
+
+def test_dp_engine_with_world_on_rccl_matches_single_process(rccl):
+    """DPEngine(HipBackend(world=World(0, 1))) on host rows with string keys:
+    the cross-rank key dictionaries, num_partitions agreement, privacy-id
+    shuffle, reduce-scatter, owner release and all-gather on RCCL, through
+    the public API; equal to HipBackend() without a world."""
+    import pipelinedp_amd as pdp
+    from pipelinedp_amd.distributed import World
+    pid, pk, val = o.synth_rows(8000, 400, 60, seed=23, zipf_s=1.1)
+    rows = [(f"user{a}", f"movie{b}", float(v)) for a, b, v in zip(pid, pk, val)]
+
+    def run(world):
+        backend = pdp.HipBackend(world=world, sampling_seed=5, noise_seed=9)
+        acct = pdp.NaiveBudgetAccountant(total_epsilon=10, total_delta=1e-3)
+        engine = pdp.DPEngine(acct, backend)
+        params = pdp.AggregateParams(metrics=[pdp.Metrics.COUNT, pdp.Metrics.SUM, pdp.Metrics.MEAN,
+                                              pdp.Metrics.PRIVACY_ID_COUNT],
+                                     max_partitions_contributed=3, max_contributions_per_partition=2,
+                                     min_value=0.0, max_value=10.0)
+        ex = pdp.DataExtractors(privacy_id_extractor=lambda r: r[0], partition_extractor=lambda r: r[1],
+                                value_extractor=lambda r: r[2])
+        res = engine.aggregate(rows, params, ex)
+        acct.compute_budgets()
+        return sorted((k, tuple(t)) for k, t in res)
+
+    want = run(None)
+    got = run(World(0, 1))
+    assert len(want) > 5
+    assert [k for k, _ in got] == [k for k, _ in want]
+    for (_, g), (_, w) in zip(got, want):
+        np.testing.assert_array_equal(g, w)
