@@ -31,6 +31,10 @@ import numpy as np  # noqa: E402
 
 import pipeline_dp  # noqa: E402  (the reference, via the stub)
 
+# The repo root holds a `pipeline_dp` alias of pipelinedp_amd: make sure the goldens come from the
+# reference and not from the implementation under test.
+assert os.path.realpath(pipeline_dp.__file__).startswith(os.path.realpath(REF) + os.sep), pipeline_dp.__file__
+
 OUT = os.path.join(REPO, "tests", "golden")
 
 METRIC = {
@@ -370,6 +374,12 @@ def analysis_cases():
     save_analysis("partition_sampling", pid, pk, val,
                   dict(metrics=["count"], L0=2, Linf=3, eps=1.0, delta=1e-6, noise_kind="laplace"),
                   sampling=0.5)
+    # G. partition sampling with public partitions: unsampled public partitions lose their rows and
+    # get the empty accumulator (contribution_bounders.py:57-66 + dp_engine.py:_add_empty_public_partitions)
+    save_analysis("public_sampling", pid, pk, val,
+                  dict(metrics=["sum", "count", "privacy_id_count"], L0=2, Linf=2, eps=1.0, delta=1e-6,
+                       noise_kind="laplace", min_sum_per_partition=-1.0, max_sum_per_partition=4.0),
+                  public=list(range(0, P, 3)) + [P + 1, P + 4], sampling=0.6)
 
 
 if __name__ == "__main__":

@@ -233,7 +233,10 @@ class AnalysisResult:
             keys = _unique_in_order(pk_raw)
         else:
             keys = raw_keys
-        if sampler is not None and self._public is None:
+        if sampler is not None:
+            # public partitions too (analysis/contribution_bounders.py:57-66 drops the rows of unsampled
+            # partitions whether or not they are public; _add_empty_public_partitions then gives the
+            # unsampled public ones the empty accumulator, while n_partitions still counts them)
             s = [k for k in keys if sampler.keep(k)]
             ns = [k for k in keys if not sampler.keep(k)]
             keys, num_sampled = s + ns, len(s)

@@ -2435,6 +2435,7 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
     HIP_TRY(hipMemcpyAsync(kc, counters, sizeof(kc), hipMemcpyDeviceToHost, stream));
     HIP_TRY(hipStreamSynchronize(stream));
     ctx->stats.k4_pairs = (int64_t)kc[kCtrK4Pairs];
+    if (kc[kCtrErr] & 2) return fail(PDP_ERR_INTERNAL, "K4 pair records not grouped by partition block");
     if (kc[kCtrErr]) return fail(PDP_ERR_INTERNAL, "radix look-back timed out (pair passes)");
   } else if (sp.packed) {
     hipLaunchKernelGGL(k_unpack_counts, dim3(grid_for(P, kThreads, 4096)), dim3(kThreads), 0, stream, acc.row_count,
