@@ -258,6 +258,64 @@ int pdp_utility_analysis_preaggregated(pdp_ctx* ctx, const int64_t* pk, const in
                                        const pdp_analysis_outputs* out, void* workspace, size_t workspace_bytes,
                                        void* stream);
 
+/* Cross-partition aggregation of the utility analysis: the device side of
+ * analysis.perform_utility_analysis (analysis/utility_analysis.py:27-161),
+ * i.e. AggregateErrorMetricsCompoundCombiner over every partition of the
+ * per-partition result (analysis/combiners.py:385-723).  Inputs are the
+ * outputs of pdp_utility_analysis (device pointers): metrics
+ * [C][nb][5][P], prob_keep [C][P] (NULL: public partitions, p = 1) and
+ * privacy_ids [P] (NULL: every partition is in the result; else only those
+ * with privacy ids -- private selection).  Outputs (device):
+ *   out_errors [C][nb][PDP_AGG_NUM_FIELDS + 2 Q]: per (configuration,
+ *     metric) the sums over partitions of the AggregateErrorMetricsAccumulator
+ *     fields (:385-416), then error_quantiles[Q], rel_error_quantiles[Q];
+ *     the caller divides as compute_metrics does (:590-640);
+ *   out_selection [C][3] (private only): partitions, sum p, sum p (1 - p)
+ *     (PrivatePartitionSelectionAggregateErrorMetricsCombiner, :677-715).
+ * As in the reference (create_accumulator, :470-480) the metric rows of
+ * every configuration weight partitions by configuration 0's keep
+ * probability.  Laplace error quantiles are the exact quantiles of
+ * Laplace(std_noise / sqrt 2) + N(0, std_cross^2), where the reference draws
+ * 10^3 Monte-Carlo samples (analysis/probability_computations.py:20-36).
+ * Sums are reduced in a fixed order (run-to-run identical).  Synchronises
+ * the stream before returning. */
+enum {
+  PDP_AGG_NUM_PARTITIONS = 0,
+  PDP_AGG_KEPT_PARTITIONS_EXPECTED = 1,
+  PDP_AGG_TOTAL_AGGREGATE = 2,
+  PDP_AGG_DATA_DROPPED_L0 = 3,
+  PDP_AGG_DATA_DROPPED_LINF = 4,
+  PDP_AGG_DATA_DROPPED_PARTITION_SELECTION = 5,
+  PDP_AGG_ERROR_L0_EXPECTED = 6,
+  PDP_AGG_ERROR_LINF_EXPECTED = 7,
+  PDP_AGG_ERROR_LINF_MIN_EXPECTED = 8,
+  PDP_AGG_ERROR_LINF_MAX_EXPECTED = 9,
+  PDP_AGG_ERROR_L0_VARIANCE = 10,
+  PDP_AGG_ERROR_VARIANCE = 11,
+  PDP_AGG_REL_ERROR_L0_EXPECTED = 12,
+  PDP_AGG_REL_ERROR_LINF_EXPECTED = 13,
+  PDP_AGG_REL_ERROR_LINF_MIN_EXPECTED = 14,
+  PDP_AGG_REL_ERROR_LINF_MAX_EXPECTED = 15,
+  PDP_AGG_REL_ERROR_L0_VARIANCE = 16,
+  PDP_AGG_REL_ERROR_VARIANCE = 17,
+  PDP_AGG_ERROR_EXPECTED_W_DROPPED = 18,
+  PDP_AGG_REL_ERROR_EXPECTED_W_DROPPED = 19,
+  PDP_AGG_NUM_FIELDS = 20,
+  PDP_AGG_MAX_QUANTILES = 8,
+};
+typedef struct pdp_aggregate_params {
+  int32_t num_configs;        /* C */
+  int32_t metrics;            /* the analysis' PDP_METRIC_* mask: blocks SUM, COUNT, PRIVACY_ID_COUNT (those set) */
+  int32_t num_quantiles;      /* Q <= PDP_AGG_MAX_QUANTILES */
+  int32_t reserved;
+  const double* quantiles;    /* [Q] host: error quantiles as perform_utility_analysis takes them (0.1, 0.5, ...) */
+  const double* std_noise;    /* [C][nb] host: SumMetrics.std_noise of each (configuration, metric) */
+  const int32_t* noise_kind;  /* [C] host: PDP_NOISE_* */
+} pdp_aggregate_params;
+int pdp_utility_aggregate(pdp_ctx* ctx, const double* metrics, const double* prob_keep, const int64_t* privacy_ids,
+                          int64_t num_partitions, const pdp_aggregate_params* params, double* out_errors,
+                          double* out_selection, void* stream);
+
 /* analysis/pre_aggregation.py:preaggregate: one (pk, count, sum, n_partitions)
  * per (privacy id, partition) of a sampled partition (pk < num_sampled), in
  * (pk, privacy id) order; out_* hold num_rows entries, *num_pairs (host) is
@@ -328,7 +386,8 @@ enum {
   PDP_STAGE_PAIR_PASS = 12,     /* K4 pair-record radix passes by partition block */
   PDP_STAGE_REDUCE = 13,        /* K4 per-partition fixed-point reduction (+ shared-block zero / finalize) */
   PDP_STAGE_ANALYSIS_SORT = 14, /* utility analysis: the (pk, pid) radix sort inside ANALYSIS_PAIRS */
-  PDP_NUM_STAGES = 15,
+  PDP_STAGE_ANALYSIS_AGGREGATE = 15, /* utility analysis: cross-partition aggregate error metrics */
+  PDP_NUM_STAGES = 16,
 };
 int pdp_profile_enable(pdp_ctx* ctx, int enable);
 /* Waits for recorded events; adds into ms_out/launches_out[PDP_NUM_STAGES]

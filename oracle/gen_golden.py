@@ -382,12 +382,120 @@ def analysis_cases():
                   public=list(range(0, P, 3)) + [P + 1, P + 4], sampling=0.6)
 
 
+def _aggregate_metrics_to_dict(am):
+    """AggregateMetrics -> {"selection": {...} | None, metric: {field: value}} (floats only)."""
+    out = {"selection": None}
+    if am.partition_selection_metrics is not None:
+        out["selection"] = {k: float(v) for k, v in vars(am.partition_selection_metrics).items()}
+    for m in ("count", "privacy_id_count", "sum"):
+        em = getattr(am, m + "_metrics", None)
+        if em is None:
+            continue
+        out[m] = {k: ([float(x) for x in v] if isinstance(v, (list, tuple, np.ndarray)) else float(v))
+                  for k, v in vars(em).items() if k != "metric_type"}
+    return out
+
+
+def run_perform_utility_analysis(rows, extractors, cfg, multi=None, public=None, pre_aggregated=False, sampling=1.0):
+    """Reference analysis.perform_utility_analysis (analysis/utility_analysis.py:27-161)
+    -> list (one per configuration) of _aggregate_metrics_to_dict."""
+    import analysis
+    kw = dict(metrics=[METRIC[m] for m in cfg["metrics"]],
+              noise_kind=pipeline_dp.NoiseKind(cfg.get("noise_kind", "laplace")),
+              max_partitions_contributed=cfg["L0"], max_contributions_per_partition=cfg["Linf"])
+    for k in ("min_sum_per_partition", "max_sum_per_partition"):
+        if cfg.get(k) is not None:
+            kw[k] = cfg[k]
+    params = pipeline_dp.AggregateParams(**kw)
+    mp = None
+    if multi:
+        mk = dict(multi)
+        if "partition_selection_strategy" in mk:
+            mk["partition_selection_strategy"] = [pipeline_dp.PartitionSelectionStrategy[v.upper()]
+                                                  for v in mk["partition_selection_strategy"]]
+        if "noise_kind" in mk:
+            mk["noise_kind"] = [pipeline_dp.NoiseKind(v) for v in mk["noise_kind"]]
+        mp = analysis.MultiParameterConfiguration(**mk)
+    options = analysis.UtilityAnalysisOptions(epsilon=cfg["eps"], delta=cfg["delta"], aggregate_params=params,
+                                              multi_param_configuration=mp, partitions_sampling_prob=sampling,
+                                              pre_aggregated_data=pre_aggregated)
+    out = list(analysis.perform_utility_analysis(rows, pipeline_dp.LocalBackend(), options, extractors,
+                                                 public_partitions=public))
+    assert len(out) == 1
+    return [_aggregate_metrics_to_dict(am) for am in out[0]]
+
+
+def save_aggregate(name, pid, pk, value, cfg, multi=None, public=None, sampling=1.0, runs=1):
+    """Golden of perform_utility_analysis.  With runs > 1 (Laplace noise: the
+    reference's error quantiles are 10^3-sample Monte-Carlo estimates,
+    analysis/probability_computations.py:20-36) the mean and the standard
+    deviation over `runs` numpy seeds are stored."""
+    rows = [(int(a), int(b), float(v)) for a, b, v in zip(pid, pk, value)]
+    ex = pipeline_dp.DataExtractors(privacy_id_extractor=lambda r: r[0], partition_extractor=lambda r: r[1],
+                                    value_extractor=lambda r: r[2])
+    res = []
+    for r in range(runs):
+        np.random.seed(1000 + r)
+        res.append(run_perform_utility_analysis(rows, ex, cfg, multi, public, sampling=sampling))
+
+    def stat(fn):
+        def walk(items):
+            first = items[0]
+            if first is None:
+                return None
+            if isinstance(first, dict):
+                return {k: walk([i[k] for i in items]) for k in first}
+            if isinstance(first, list):
+                return [walk([i[j] for i in items]) for j in range(len(first))]
+            return fn(np.asarray(items, np.float64))
+        return walk(res)
+
+    expected = stat(lambda a: float(a.mean()))
+    spread = stat(lambda a: float(a.std(ddof=1)) if len(a) > 1 else 0.0)
+    np.savez_compressed(
+        os.path.join(OUT, "aggregate_" + name + ".npz"),
+        pid=np.asarray(pid, np.int64), pk=np.asarray(pk, np.int64), value=np.asarray(value, np.float64),
+        public=np.asarray(public if public is not None else [], np.int64), has_public=np.asarray(public is not None),
+        meta=np.asarray(json.dumps(dict(cfg=cfg, multi=multi, sampling=sampling, runs=runs, expected=expected,
+                                        spread=spread))))
+    print(f"aggregate_{name}: {len(expected)} configurations, runs={runs}")
+
+
+def aggregate_cases():
+    """perform_utility_analysis goldens (cross-partition aggregate error metrics)."""
+    rng = np.random.default_rng(20251017)
+    n, U, P = 6000, 500, 50
+    pid = rng.integers(0, U, n)
+    pk = np.minimum(rng.zipf(1.5, n) - 1, P - 1)
+    val = rng.normal(2.0, 3.0, n)
+    # private selection, Gaussian noise (deterministic: norm.ppf quantiles), 4 configurations
+    save_aggregate("private_gaussian", pid, pk, val,
+                   dict(metrics=["count", "sum", "privacy_id_count"], L0=2, Linf=2, eps=3.0, delta=1e-5,
+                        noise_kind="gaussian", min_sum_per_partition=-3.0, max_sum_per_partition=5.0),
+                   multi=dict(max_partitions_contributed=[1, 2, 3, 5], max_contributions_per_partition=[1, 2, 3, 1],
+                              min_sum_per_partition=[-3.0, 0.0, -1.0, 1.0],
+                              max_sum_per_partition=[5.0, 2.0, 4.0, 3.0]))
+    # public partitions (absent ones too), Gaussian
+    save_aggregate("public_gaussian", pid, pk, val,
+                   dict(metrics=["sum", "count"], L0=3, Linf=2, eps=1.0, delta=1e-6, noise_kind="gaussian",
+                        min_sum_per_partition=0.5, max_sum_per_partition=6.0),
+                   public=list(range(0, P, 2)) + [P + 3, P + 9])
+    # Laplace noise: Monte-Carlo quantiles in the reference -> mean / std over 16 seeds
+    save_aggregate("private_laplace", pid, pk, val,
+                   dict(metrics=["count", "privacy_id_count"], L0=2, Linf=2, eps=2.0, delta=1e-5,
+                        noise_kind="laplace"),
+                   multi=dict(max_partitions_contributed=[1, 3], max_contributions_per_partition=[2, 1]), runs=16)
+
+
 if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "select":
         select_partitions_cases()
     elif len(sys.argv) > 1 and sys.argv[1] == "analysis":
         analysis_cases()
+    elif len(sys.argv) > 1 and sys.argv[1] == "aggregate":
+        aggregate_cases()
     else:
         main()
         select_partitions_cases()
         analysis_cases()
+        aggregate_cases()

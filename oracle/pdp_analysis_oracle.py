@@ -201,3 +201,165 @@ def noise_std(kind, eps, delta, l0, linf):
     if kind == "laplace":
         return l0 * linf / eps * math.sqrt(2)
     return o.gaussian_sigma(eps, delta, math.sqrt(l0) * linf)
+
+
+# ---------------------------------------------------------------------------
+# Cross-partition aggregation: perform_utility_analysis
+# (analysis/utility_analysis.py:27-161) -- the AggregateErrorMetricsCompoundCombiner
+# over every partition's per-partition metrics (analysis/combiners.py:385-723).
+# ---------------------------------------------------------------------------
+
+ERROR_QUANTILES = (0.1, 0.5, 0.9, 0.99)  # utility_analysis.py:68
+# AggregateErrorMetricsAccumulator fields summed over partitions (combiners.py:385-416), quantile
+# lists excluded (they follow as 2 x Q entries: error_quantiles, rel_error_quantiles)
+ACC_FIELDS = ("num_partitions", "kept_partitions_expected", "total_aggregate", "data_dropped_l0",
+              "data_dropped_linf", "data_dropped_partition_selection", "error_l0_expected", "error_linf_expected",
+              "error_linf_min_expected", "error_linf_max_expected", "error_l0_variance", "error_variance",
+              "rel_error_l0_expected", "rel_error_linf_expected", "rel_error_linf_min_expected",
+              "rel_error_linf_max_expected", "rel_error_l0_variance", "rel_error_variance",
+              "error_expected_w_dropped_partitions", "rel_error_expected_w_dropped_partitions")
+
+
+def _ndtr(z):
+    from scipy.special import ndtr
+    return ndtr(z)
+
+
+def laplace_gaussian_cdf(x, b, sigma):
+    """CDF of Laplace(0, b) + N(0, sigma^2) at x: E[F_L(x - G)] in closed form,
+    the two exponential terms taken as erfcx products so nothing overflows."""
+    from scipy.special import erfcx
+    x = np.asarray(x, np.float64)
+    if sigma == 0:
+        return np.where(x < 0, 0.5 * np.exp(np.minimum(x, 0) / b), 1 - 0.5 * np.exp(-np.maximum(x, 0) / b))
+    if b == 0:
+        return _ndtr(x / sigma)
+    r = sigma / b
+    u = x / sigma
+    g = np.exp(-0.5 * u * u)
+    with np.errstate(over="ignore", invalid="ignore"):  # np.where evaluates both branches
+        return _lg_cdf(x, b, r, u, g)
+
+
+def _lg_cdf(x, b, r, u, g):
+    from scipy.special import erfcx
+    # 1/2 e^{r^2/2 - x/b} Phi(u - r)  and  1/2 e^{r^2/2 + x/b} Phi(-u - r)
+    t2 = np.where(u - r < 0, 0.25 * erfcx((r - u) / math.sqrt(2)) * g,
+                  0.5 * np.exp(0.5 * r * r - x / b) * _ndtr(u - r))
+    t3 = np.where(u + r > 0, 0.25 * erfcx((u + r) / math.sqrt(2)) * g,
+                  0.5 * np.exp(0.5 * r * r + x / b) * _ndtr(-u - r))
+    return _ndtr(u) - t2 + t3
+
+
+def laplace_gaussian_quantile(q, b, sigma):
+    """The exact q-quantile of Laplace(0, b) + N(0, sigma^2), by bisection on
+    laplace_gaussian_cdf.  The reference estimates it from 10^3 Monte-Carlo
+    samples (analysis/probability_computations.py:20-36); this is the value
+    that estimate converges to."""
+    if sigma == 0:
+        return b * math.log(2 * q) if q < 0.5 else -b * math.log(2 * (1 - q))
+    if b == 0:
+        from scipy.special import ndtri
+        return sigma * float(ndtri(q))
+    lo, hi = -(40 * b + 40 * sigma), 40 * b + 40 * sigma
+    for _ in range(200):
+        mid = 0.5 * (lo + hi)
+        if laplace_gaussian_cdf(mid, b, sigma) < q:
+            lo = mid
+        else:
+            hi = mid
+        if hi - lo <= 1e-15 * max(1.0, abs(mid)):
+            break
+    return 0.5 * (lo + hi)
+
+
+def error_quantile_values(kind, expected_cross, std_cross, std_noise, quantiles):
+    """SumAggregateErrorMetricsCombiner._compute_error_quantiles' distribution
+    quantiles (combiners.py:655-674) before the per-partition error is added:
+    Gaussian: norm.ppf(q, E, sqrt(std_cross^2 + std_noise^2)); Laplace: the
+    Laplace(std_noise / sqrt 2) + N(0, std_cross^2) quantile (exact here, see
+    laplace_gaussian_quantile; the reference's Laplace values ignore E)."""
+    if kind == "gaussian":
+        from scipy.special import ndtri
+        s = math.sqrt(std_cross**2 + std_noise**2)
+        return [expected_cross + s * float(ndtri(q)) for q in quantiles]
+    return [laplace_gaussian_quantile(q, std_noise / math.sqrt(2), std_cross) for q in quantiles]
+
+
+def aggregate_accumulator(metric, per_part, prob_keep, std_noise, kind, quantiles=ERROR_QUANTILES):
+    """Sum over partitions of SumAggregateErrorMetricsCombiner.create_accumulator
+    (combiners.py:497-585) for one configuration and metric.  per_part: [5, P]
+    (FIELDS), prob_keep: [P] or None (public partitions: 1).  -> dict of
+    ACC_FIELDS plus "error_quantiles" / "rel_error_quantiles" lists."""
+    inv = [1 - q for q in quantiles]  # _invert_error_quantiles
+    P = per_part.shape[1]
+    acc = {f: 0.0 for f in ACC_FIELDS}
+    acc["error_quantiles"] = [0.0] * len(inv)
+    acc["rel_error_quantiles"] = [0.0] * len(inv)
+    for p in range(P):
+        s, emin, emax, ecross, var_cross = (float(v) for v in per_part[:, p])
+        std_cross = math.sqrt(max(var_cross, 0.0))
+        pk = 1.0 if prob_keep is None else float(prob_keep[p])
+        t = {"num_partitions": 1.0, "kept_partitions_expected": pk, "total_aggregate": s}
+        if metric != "sum":
+            t["data_dropped_l0"] = -ecross
+            t["data_dropped_linf"] = -emax
+            t["data_dropped_partition_selection"] = (1 - pk) * (s + ecross + emax)
+        t["error_l0_expected"] = pk * ecross
+        t["error_linf_min_expected"] = pk * emin
+        t["error_linf_max_expected"] = pk * emax
+        t["error_linf_expected"] = t["error_linf_min_expected"] + t["error_linf_max_expected"]
+        t["error_l0_variance"] = pk * std_cross**2
+        t["error_variance"] = pk * (std_cross**2 + std_noise**2)
+        eq = [pk * (v + emin + emax) for v in error_quantile_values(kind, ecross, std_cross, std_noise, inv)]
+        t["error_expected_w_dropped_partitions"] = pk * (ecross + emin + emax) + (1 - pk) * -s
+        if s != 0:
+            a = abs(s)
+            for f in ("l0_expected", "linf_min_expected", "linf_max_expected"):
+                t["rel_error_" + f] = t["error_" + f] / a
+            t["rel_error_linf_expected"] = t["rel_error_linf_min_expected"] + t["rel_error_linf_max_expected"]
+            t["rel_error_l0_variance"] = t["error_l0_variance"] / s**2
+            t["rel_error_variance"] = t["error_variance"] / s**2
+            t["rel_error_expected_w_dropped_partitions"] = t["error_expected_w_dropped_partitions"] / a
+            req = [e / a for e in eq]
+        else:
+            req = [0.0] * len(eq)
+        for f, v in t.items():
+            acc[f] += v
+        acc["error_quantiles"] = [x + y for x, y in zip(acc["error_quantiles"], eq)]
+        acc["rel_error_quantiles"] = [x + y for x, y in zip(acc["rel_error_quantiles"], req)]
+    return acc
+
+
+def aggregate_error_metrics(acc, std_noise):
+    """SumAggregateErrorMetricsCombiner.compute_metrics (combiners.py:590-640)
+    -> dict of AggregateErrorMetrics fields (metric_type excluded)."""
+    k = acc["kept_partitions_expected"]
+    total = max(1.0, acc["total_aggregate"])
+    out = {"ratio_data_dropped_l0": acc["data_dropped_l0"] / total,
+           "ratio_data_dropped_linf": acc["data_dropped_linf"] / total,
+           "ratio_data_dropped_partition_selection": acc["data_dropped_partition_selection"] / total}
+    for pre in ("", "rel_"):
+        l0 = acc[pre + "error_l0_expected"] / k
+        lmin = acc[pre + "error_linf_min_expected"] / k
+        lmax = acc[pre + "error_linf_max_expected"] / k
+        out[pre + "error_l0_expected"] = l0
+        out[pre + "error_linf_expected"] = lmin + lmax
+        out[pre + "error_linf_min_expected"] = lmin
+        out[pre + "error_linf_max_expected"] = lmax
+        out[pre + "error_expected"] = l0 + lmin + lmax
+        out[pre + "error_l0_variance"] = acc[pre + "error_l0_variance"] / k
+        out[pre + "error_variance"] = acc[pre + "error_variance"] / k
+        out[pre + "error_quantiles"] = [v / k for v in acc[pre + "error_quantiles"]]
+        out[pre + "error_expected_w_dropped_partitions"] = (acc[pre + "error_expected_w_dropped_partitions"] /
+                                                            acc["num_partitions"])
+    out["noise_std"] = std_noise
+    return out
+
+
+def partition_selection_metrics(prob_keep):
+    """PrivatePartitionSelectionAggregateErrorMetricsCombiner.compute_metrics
+    (combiners.py:700-715) over the moments of the keep indicators (:87-96)."""
+    p = np.asarray(prob_keep, np.float64)
+    return {"num_partitions": len(p), "dropped_partitions_expected": len(p) - float(np.sum(p)),
+            "dropped_partitions_variance": float(np.sum(p * (1 - p)))}

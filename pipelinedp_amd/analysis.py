@@ -15,11 +15,16 @@ Poisson-binomial keep probability of private partition selection -- runs in
 libpdp_hip.so (``pdp_utility_analysis``, include/pdp_hip.h).  The noise
 standard deviation is host arithmetic (dp_computations.py:462-481).
 
-Not built: the cross-partition aggregation of perform_utility_analysis
-(AggregateErrorMetrics with Monte-Carlo error quantiles) and parameter
-tuning -- DESIGN.md, out of scope.
+``perform_utility_analysis`` (analysis/utility_analysis.py:27-161) adds the
+cross-partition aggregation on the device (``pdp_utility_aggregate``): the
+sums of AggregateErrorMetricsCompoundCombiner's accumulators over every
+partition, divided here as compute_metrics does (analysis/combiners.py:
+590-640, 700-715).  Laplace error quantiles are exact (closed-form CDF of
+Laplace + Gaussian, inverted on the GPU) where the reference uses 10^3
+Monte-Carlo samples.  Parameter tuning is out of scope.
 """
 import copy
+import enum
 import dataclasses
 import hashlib
 import math
@@ -198,6 +203,13 @@ class AnalysisResult:
         return cfgs
 
     def _encode_and_run(self):
+        """The device run behind the result, once (per-partition tuples and the
+        cross-partition aggregation share it)."""
+        if getattr(self, "_raw", None) is None:
+            self._raw = self._encode_and_run_once()
+        return self._raw
+
+    def _encode_and_run_once(self):
         backend = self._engine._backend
         ex = backend.executor
         torch = ex.torch
@@ -389,3 +401,180 @@ def preaggregate(col, data_extractors, partitions_sampling_prob: float = 1, devi
                             num_sampled)
     ppk, cnt, sm, npart = (a.cpu().numpy() for a in pairs)
     return [(keys[k], (int(c), float(s), int(n))) for k, c, s, n in zip(ppk, cnt, sm, npart)]
+
+
+# ---------------------------------------------------------------------------
+# Cross-partition aggregation (perform_utility_analysis)
+# ---------------------------------------------------------------------------
+
+
+class AggregateMetricType(enum.Enum):
+    """analysis/metrics.py:51-54."""
+    PRIVACY_ID_COUNT = 'privacy_id_count'
+    COUNT = 'count'
+    SUM = 'sum'
+
+
+@dataclasses.dataclass
+class AggregateErrorMetrics:
+    """Cross-partition error metrics of one aggregation (analysis/metrics.py:57-120):
+    averages over partitions weighted by the keep probability, except the
+    ratio_* fields (ratios of the totals) and the *_w_dropped_partitions ones
+    (averages over all partitions)."""
+    metric_type: AggregateMetricType
+    ratio_data_dropped_l0: float
+    ratio_data_dropped_linf: float
+    ratio_data_dropped_partition_selection: float
+    error_l0_expected: float
+    error_linf_expected: float
+    error_linf_min_expected: float
+    error_linf_max_expected: float
+    error_expected: float
+    error_l0_variance: float
+    error_variance: float
+    error_quantiles: List[float]
+    rel_error_l0_expected: float
+    rel_error_linf_expected: float
+    rel_error_linf_min_expected: float
+    rel_error_linf_max_expected: float
+    rel_error_expected: float
+    rel_error_l0_variance: float
+    rel_error_variance: float
+    rel_error_quantiles: List[float]
+    error_expected_w_dropped_partitions: float
+    rel_error_expected_w_dropped_partitions: float
+    noise_std: float
+
+    def absolute_rmse(self) -> float:
+        return math.sqrt(self.error_expected**2 + self.error_variance)
+
+    def relative_rmse(self) -> float:
+        return math.sqrt(self.rel_error_expected**2 + self.rel_error_variance)
+
+
+@dataclasses.dataclass
+class PartitionSelectionMetrics:
+    """analysis/metrics.py:123-129."""
+    num_partitions: float
+    dropped_partitions_expected: float
+    dropped_partitions_variance: float
+
+
+@dataclasses.dataclass
+class AggregateMetrics:
+    """Utility analysis result for one configuration (analysis/metrics.py:132-150)."""
+    input_aggregate_params: agg.AggregateParams
+    count_metrics: Optional[AggregateErrorMetrics] = None
+    privacy_id_count_metrics: Optional[AggregateErrorMetrics] = None
+    partition_selection_metrics: Optional[PartitionSelectionMetrics] = None
+    sum_metrics: Optional[AggregateErrorMetrics] = None
+
+
+ERROR_QUANTILES = (0.1, 0.5, 0.9, 0.99)  # utility_analysis.py:68
+_METRIC_TYPE = {agg.Metrics.SUM: AggregateMetricType.SUM, agg.Metrics.COUNT: AggregateMetricType.COUNT,
+                agg.Metrics.PRIVACY_ID_COUNT: AggregateMetricType.PRIVACY_ID_COUNT}
+
+
+def _error_metrics(metric_type, acc, Q, std_noise) -> AggregateErrorMetrics:
+    """SumAggregateErrorMetricsCombiner.compute_metrics (combiners.py:590-640)
+    on one row of pdp_utility_aggregate's sums."""
+    f = dict(zip(native.AGG_FIELDS, (float(v) for v in acc[:native.AGG_NUM_FIELDS])))
+    eq = [float(v) for v in acc[native.AGG_NUM_FIELDS:native.AGG_NUM_FIELDS + Q]]
+    req = [float(v) for v in acc[native.AGG_NUM_FIELDS + Q:native.AGG_NUM_FIELDS + 2 * Q]]
+    k = f["kept_partitions_expected"]
+    total = max(1.0, f["total_aggregate"])
+    l0, lmin, lmax = f["error_l0_expected"] / k, f["error_linf_min_expected"] / k, f["error_linf_max_expected"] / k
+    rl0 = f["rel_error_l0_expected"] / k
+    rlmin, rlmax = f["rel_error_linf_min_expected"] / k, f["rel_error_linf_max_expected"] / k
+    n = f["num_partitions"]
+    return AggregateErrorMetrics(
+        metric_type=metric_type,
+        ratio_data_dropped_l0=f["data_dropped_l0"] / total,
+        ratio_data_dropped_linf=f["data_dropped_linf"] / total,
+        ratio_data_dropped_partition_selection=f["data_dropped_partition_selection"] / total,
+        error_l0_expected=l0, error_linf_expected=lmin + lmax, error_linf_min_expected=lmin,
+        error_linf_max_expected=lmax, error_expected=l0 + lmin + lmax,
+        error_l0_variance=f["error_l0_variance"] / k, error_variance=f["error_variance"] / k,
+        error_quantiles=[v / k for v in eq],
+        rel_error_l0_expected=rl0, rel_error_linf_expected=rlmin + rlmax, rel_error_linf_min_expected=rlmin,
+        rel_error_linf_max_expected=rlmax, rel_error_expected=rl0 + rlmin + rlmax,
+        rel_error_l0_variance=f["rel_error_l0_variance"] / k, rel_error_variance=f["rel_error_variance"] / k,
+        rel_error_quantiles=[v / k for v in req],
+        error_expected_w_dropped_partitions=f["error_expected_w_dropped_partitions"] / n,
+        rel_error_expected_w_dropped_partitions=f["rel_error_expected_w_dropped_partitions"] / n,
+        noise_std=std_noise)
+
+
+class AggregateResult:
+    """Lazy one-element collection holding the list of AggregateMetrics (one
+    per configuration), as perform_utility_analysis returns it."""
+
+    def __init__(self, per_partition: "AnalysisResult", quantiles):
+        self._pp = per_partition
+        self._quantiles = list(quantiles)
+        self._out = None
+
+    def __iter__(self):
+        if self._out is None:
+            self._out = [self._pp._aggregate(self._quantiles)]
+        return iter(self._out)
+
+
+def _aggregate(self, quantiles):
+    """AnalysisResult -> [AggregateMetrics per configuration] via
+    pdp_utility_aggregate on the device arrays of the per-partition result."""
+    keys, metrics, prob, pids, _ = self._encode_and_run()
+    opts = self._options
+    params_list = get_aggregate_params(opts)
+    present = [m for m in _ANALYSIS_METRICS if m in opts.aggregate_params.metrics]
+    private = self._public is None
+    C, Q = len(params_list), len(quantiles)
+    stds = [[noise_std(p, self._metric_specs[m].eps, self._metric_specs[m].delta) for m in present]
+            for p in params_list]
+    if metrics is None or len(keys) == 0:
+        raise ValueError("utility analysis over an empty partition set")
+    kinds = [native.NOISE_GAUSSIAN if p.noise_kind == agg.NoiseKind.GAUSSIAN else native.NOISE_LAPLACE
+             for p in params_list]
+    mask = sum(bit for m, bit in ((agg.Metrics.SUM, native.METRIC_SUM), (agg.Metrics.COUNT, native.METRIC_COUNT),
+                                  (agg.Metrics.PRIVACY_ID_COUNT, native.METRIC_PRIVACY_ID_COUNT))
+               if m in opts.aggregate_params.metrics)
+    errors, sel = self._engine._backend.executor.aggregate_errors(metrics, prob, pids, mask, stds, kinds, quantiles,
+                                                                  private)
+    errors = errors.cpu().numpy()
+    sel = sel.cpu().numpy() if sel is not None else None
+    out = []
+    for c, p in enumerate(params_list):
+        am = AggregateMetrics(input_aggregate_params=p)
+        if private:
+            n, e, v = (float(x) for x in sel[c])
+            am.partition_selection_metrics = PartitionSelectionMetrics(num_partitions=n,
+                                                                       dropped_partitions_expected=n - e,
+                                                                       dropped_partitions_variance=v)
+        for b, m in enumerate(present):
+            em = _error_metrics(_METRIC_TYPE[m], errors[c, b], Q, stds[c][b])
+            setattr(am, {agg.Metrics.SUM: "sum_metrics", agg.Metrics.COUNT: "count_metrics",
+                         agg.Metrics.PRIVACY_ID_COUNT: "privacy_id_count_metrics"}[m], em)
+        out.append(am)
+    return out
+
+
+AnalysisResult._aggregate = _aggregate
+
+
+def perform_utility_analysis(col, backend, options: UtilityAnalysisOptions, data_extractors, public_partitions=None,
+                             return_per_partition: bool = False):
+    """Utility analysis of DP aggregations (analysis/utility_analysis.py:27-119):
+    the per-partition analysis of UtilityAnalysisEngine, then its
+    cross-partition aggregation.  Returns a one-element collection holding
+    the list of AggregateMetrics (one per configuration); with
+    return_per_partition, (that collection, the per-partition result)."""
+    from .budget_accounting import NaiveBudgetAccountant
+    accountant = NaiveBudgetAccountant(total_epsilon=options.epsilon, total_delta=options.delta)
+    engine = UtilityAnalysisEngine(budget_accountant=accountant, backend=backend)
+    per_partition = engine.analyze(col, options=options, data_extractors=data_extractors,
+                                   public_partitions=public_partitions)
+    accountant.compute_budgets()
+    result = AggregateResult(per_partition, ERROR_QUANTILES)
+    if return_per_partition:
+        return result, per_partition
+    return result

@@ -848,6 +848,7 @@ __device__ __forceinline__ void emit_group(const SegParams& sp, const AccPtrs& a
 #include "pdp_segments.inc"
 #include "pdp_thin.inc"
 #include "pdp_analysis.inc"
+#include "pdp_aggregate.inc"
 
 // ---------------------------------------------------------------------------
 // KF: generic sorted-stream path (fallback for buckets that overflow LDS)
@@ -2868,6 +2869,78 @@ int pdp_utility_analysis(pdp_ctx* ctx, const pdp_columns* cols, int64_t num_samp
   return analysis_impl(ctx, cols->pid, cols->pk, cols->value, nullptr, nullptr, cols->num_rows,
                        cols->num_privacy_ids, cols->num_partitions, num_sampled_partitions, metrics, cfgs, num_configs,
                        out, workspace, workspace_bytes, (hipStream_t)stream);
+}
+
+int pdp_utility_aggregate(pdp_ctx* ctx, const double* metrics, const double* prob_keep, const int64_t* privacy_ids,
+                          int64_t num_partitions, const pdp_aggregate_params* ap, double* out_errors,
+                          double* out_selection, void* stream_) {
+  if (!ctx || !ap || !out_errors) return fail(PDP_ERR_INVALID_ARG, "null argument");
+  const int C = ap->num_configs, Q = ap->num_quantiles;
+  const int mflags = ap->metrics & (PDP_METRIC_SUM | PDP_METRIC_COUNT | PDP_METRIC_PRIVACY_ID_COUNT);
+  const int nb = ((mflags & PDP_METRIC_SUM) != 0) + ((mflags & PDP_METRIC_COUNT) != 0) +
+                 ((mflags & PDP_METRIC_PRIVACY_ID_COUNT) != 0);
+  if (C < 1 || nb < 1 || mflags != ap->metrics) return fail(PDP_ERR_INVALID_ARG, "bad configuration / metric count");
+  if (Q < 0 || Q > PDP_AGG_MAX_QUANTILES || (Q > 0 && !ap->quantiles))
+    return fail(PDP_ERR_INVALID_ARG, "num_quantiles must be in [0, 8]");
+  if (!ap->std_noise || !ap->noise_kind) return fail(PDP_ERR_INVALID_ARG, "std_noise / noise_kind required");
+  if (num_partitions < 0 || (num_partitions > 0 && !metrics)) return fail(PDP_ERR_INVALID_ARG, "metrics required");
+  if (prob_keep && !out_selection) return fail(PDP_ERR_INVALID_ARG, "out_selection required with prob_keep");
+  for (int j = 0; j < Q; ++j)
+    if (!(ap->quantiles[j] > 0.0 && ap->quantiles[j] < 1.0)) return fail(PDP_ERR_INVALID_ARG, "quantiles in (0, 1)");
+  for (int c = 0; c < C; ++c)
+    if (ap->noise_kind[c] != PDP_NOISE_LAPLACE && ap->noise_kind[c] != PDP_NOISE_GAUSSIAN)
+      return fail(PDP_ERR_INVALID_ARG, "Noise kind must be either Laplace or Gaussian.");
+  DeviceGuard dg(ctx->device);
+  if (!dg.ok) return fail(PDP_ERR_HIP, "hipSetDevice failed");
+  hipStream_t stream = (hipStream_t)stream_;
+  const int K = kAggFields + 2 * Q;
+  const int nerr = C * nb, nsel = prob_keep ? C : 0, nrows = nerr + nsel;
+  const int64_t P = num_partitions;
+  // metric blocks in pdp_utility_analysis order: SUM, COUNT, PRIVACY_ID_COUNT (those present)
+  int is_sum[3], b = 0;
+  for (int m : {PDP_METRIC_SUM, PDP_METRIC_COUNT, PDP_METRIC_PRIVACY_ID_COUNT})
+    if (mflags & m) is_sum[b++] = m == PDP_METRIC_SUM;
+  std::vector<AggRow> rows((size_t)nrows);
+  for (int c = 0; c < C; ++c)
+    for (int k = 0; k < nb; ++k) {
+      AggRow& r = rows[(size_t)c * nb + k];
+      r.m = metrics + ((size_t)c * nb + k) * 5 * (size_t)P;
+      r.prob = prob_keep;  // configuration 0's (combiners.py:470-480)
+      r.std_noise = ap->std_noise[(size_t)c * nb + k];
+      r.kind = ap->noise_kind[c];
+      r.is_sum = is_sum[k];
+    }
+  for (int c = 0; c < nsel; ++c) {
+    AggRow& r = rows[(size_t)nerr + c];
+    r.m = nullptr;
+    r.prob = prob_keep + (size_t)c * P;
+  }
+  AggParams prm{};
+  prm.nrows = nrows;
+  prm.K = K;
+  prm.Q = Q;
+  for (int j = 0; j < Q; ++j) prm.q[j] = 1.0 - ap->quantiles[j];  // _invert_error_quantiles
+  prm.privacy_ids = privacy_ids;
+  prm.P = P;
+  const int nblocks = (int)std::max<int64_t>(1, std::min<int64_t>((P + kAggThreads - 1) / kAggThreads, kAggMaxBlocks));
+  AsyncFrees scratch(stream);
+  AggRow* d_rows = nullptr;
+  double* partials = nullptr;
+  HIP_TRY(scratch.alloc((void**)&d_rows, rows.size() * sizeof(AggRow)));
+  HIP_TRY(scratch.alloc((void**)&partials, (size_t)nrows * nblocks * kAggMaxK * sizeof(double)));
+  HIP_TRY(hipMemcpyAsync(d_rows, rows.data(), rows.size() * sizeof(AggRow), hipMemcpyHostToDevice, stream));
+  prm.rows = d_rows;
+  {
+    ProfScope ps(ctx, PDP_STAGE_ANALYSIS_AGGREGATE, stream);
+    hipLaunchKernelGGL(k_agg_partials, dim3((unsigned)nblocks, (unsigned)nrows), dim3(kAggThreads), 0, stream, prm,
+                       partials);
+    const int tot = nrows * kAggMaxK;
+    hipLaunchKernelGGL(k_agg_final, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, stream, partials, nerr, nsel,
+                       nblocks, K, out_errors, out_selection);
+  }
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(stream));  // `rows` (host) is read by the copy above
+  return 0;
 }
 
 int pdp_utility_analysis_preaggregated(pdp_ctx* ctx, const int64_t* pk, const int64_t* count, const double* sum,

@@ -41,6 +41,9 @@ class ReleaseConfig:
     noise_seed: Optional[int] = None
 
 
+c_void = ctypes.c_void_p
+
+
 def _ptr(t):
     return ctypes.c_void_p(t.data_ptr()) if t is not None else None
 
@@ -225,6 +228,29 @@ class HipExecutor:
                                                        ctypes.byref(outs), ctypes.c_void_p(ws.data_ptr()), ws.numel(),
                                                        self.stream_handle), "pdp_utility_analysis")
         return metrics, prob, pids
+
+    def aggregate_errors(self, metrics, prob_keep, privacy_ids, metrics_mask: int, std_noise, noise_kinds,
+                         quantiles, private: bool):
+        """pdp_utility_aggregate: cross-partition sums of the per-partition
+        utility metrics (analyze's outputs) -> (errors [C, nb, 20 + 2Q],
+        selection [C, 3] or None) device tensors; field order native.AGG_FIELDS,
+        then error_quantiles[Q], rel_error_quantiles[Q]."""
+        torch = self.torch
+        C, nb, _, P = (int(v) for v in metrics.shape)
+        Q = len(quantiles)
+        errors = torch.empty((C, nb, native.AGG_NUM_FIELDS + 2 * Q), dtype=torch.float64, device=self.device)
+        sel = torch.empty((C, 3), dtype=torch.float64, device=self.device) if private else None
+        qs = (ctypes.c_double * max(Q, 1))(*quantiles)
+        sn = (ctypes.c_double * (C * nb))(*[float(v) for row in std_noise for v in row])
+        nk = (ctypes.c_int32 * C)(*noise_kinds)
+        ap = native.AggregateParams(C, metrics_mask, Q, 0, ctypes.cast(qs, c_void), ctypes.cast(sn, c_void),
+                                    ctypes.cast(nk, c_void))
+        native.check(self.lib.pdp_utility_aggregate(self.ctx, _ptr(metrics.contiguous()),
+                                                    _ptr(prob_keep) if private else None,
+                                                    _ptr(privacy_ids) if private else None, P, ctypes.byref(ap),
+                                                    _ptr(errors), _ptr(sel), self.stream_handle),
+                     "pdp_utility_aggregate")
+        return errors, sel
 
     def preaggregate(self, pid, pk, value, num_privacy_ids: int, num_partitions: int,
                      num_sampled_partitions: Optional[int] = None):

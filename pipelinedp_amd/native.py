@@ -64,6 +64,20 @@ class AnalysisOutputs(ctypes.Structure):
     _fields_ = [("metrics", c_vp), ("prob_keep", c_vp), ("privacy_ids", c_vp)]
 
 
+class AggregateParams(ctypes.Structure):
+    _fields_ = [("num_configs", c_i32), ("metrics", c_i32), ("num_quantiles", c_i32), ("reserved", c_i32),
+                ("quantiles", c_vp), ("std_noise", c_vp), ("noise_kind", c_vp)]
+
+
+AGG_NUM_FIELDS = 20  # PDP_AGG_NUM_FIELDS; field order = pdp_hip.h PDP_AGG_* enum
+AGG_FIELDS = ("num_partitions", "kept_partitions_expected", "total_aggregate", "data_dropped_l0",
+              "data_dropped_linf", "data_dropped_partition_selection", "error_l0_expected", "error_linf_expected",
+              "error_linf_min_expected", "error_linf_max_expected", "error_l0_variance", "error_variance",
+              "rel_error_l0_expected", "rel_error_linf_expected", "rel_error_linf_min_expected",
+              "rel_error_linf_max_expected", "rel_error_l0_variance", "rel_error_variance",
+              "error_expected_w_dropped_partitions", "rel_error_expected_w_dropped_partitions")
+
+
 class Stats(ctypes.Structure):
     _fields_ = [("kept_rows_in", c_i64), ("fallback_rows", c_i64), ("fallback_ranges", c_i64),
                 ("sort_passes", c_i32), ("bucket_low_bits", c_i32), ("sweep_cycles", c_i64 * 4),
@@ -96,6 +110,8 @@ SIGNATURES = [
                                             ctypes.POINTER(ctypes.c_size_t)]),
     ("pdp_utility_analysis", c_i32, [c_vp, ctypes.POINTER(Columns), c_i64, c_i32, ctypes.POINTER(AnalysisConfig),
                                      c_i32, ctypes.POINTER(AnalysisOutputs), c_vp, ctypes.c_size_t, c_vp]),
+    ("pdp_utility_aggregate", c_i32, [c_vp, c_vp, c_vp, c_vp, c_i64, ctypes.POINTER(AggregateParams), c_vp, c_vp,
+                                      c_vp]),
     ("pdp_utility_analysis_preaggregated", c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i64, c_i32,
                                                    ctypes.POINTER(AnalysisConfig), c_i32,
                                                    ctypes.POINTER(AnalysisOutputs), c_vp, ctypes.c_size_t, c_vp]),
@@ -114,7 +130,7 @@ SIGNATURES = [
 
 STAGES = ["histogram", "onesweep_first", "onesweep_rest", "buckets", "generic", "release", "enforced",
           "tile_counts", "analysis_pairs", "analysis_metrics", "filter", "survivor_sort", "pair_pass", "reduce",
-          "analysis_sort"]
+          "analysis_sort", "analysis_aggregate"]
 
 _lib = None
 

@@ -110,3 +110,29 @@ class CpuExecutor:
         prob = None if public else torch.from_numpy(out["prob_keep"])
         pids = np.bincount(pairs[0], minlength=P).astype(np.int64)
         return torch.from_numpy(metrics), prob, torch.from_numpy(pids)
+
+    def aggregate_errors(self, metrics, prob_keep, privacy_ids, metrics_mask, std_noise, noise_kinds, quantiles,
+                         private):
+        """pdp_utility_aggregate restated with pdp_analysis_oracle.aggregate_accumulator."""
+        import pdp_analysis_oracle as ao
+        torch = self.torch
+        m = metrics.numpy()
+        C, nb, _, P = m.shape
+        names = [n for n, bit in (("sum", native.METRIC_SUM), ("count", native.METRIC_COUNT),
+                                  ("privacy_id_count", native.METRIC_PRIVACY_ID_COUNT)) if metrics_mask & bit]
+        present = np.flatnonzero(privacy_ids.numpy() > 0) if private else np.arange(P)
+        prob = prob_keep.numpy() if private else None
+        Q = len(quantiles)
+        errors = np.zeros((C, nb, native.AGG_NUM_FIELDS + 2 * Q))
+        for c in range(C):
+            kind = "gaussian" if noise_kinds[c] == native.NOISE_GAUSSIAN else "laplace"
+            for b, name in enumerate(names):
+                acc = ao.aggregate_accumulator(name, m[c, b][:, present], None if prob is None else prob[0, present],
+                                               std_noise[c][b], kind, tuple(quantiles))
+                errors[c, b] = [acc[f] for f in ao.ACC_FIELDS] + acc["error_quantiles"] + acc["rel_error_quantiles"]
+        sel = None
+        if private:
+            sel = np.array([[len(present), prob[c, present].sum(), (prob[c, present] * (1 - prob[c, present])).sum()]
+                            for c in range(C)])
+            sel = torch.from_numpy(sel)
+        return torch.from_numpy(errors), sel

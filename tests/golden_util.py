@@ -17,7 +17,7 @@ def load(name):
 
 def aggregate_cases():
     names = sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN, "*.npz")))
-    return [n for n in names if not n.startswith(("binding_", "select_partitions_", "analysis_"))]
+    return [n for n in names if not n.startswith(("binding_", "select_partitions_", "analysis_", "aggregate_"))]
 
 
 def known_answers():

@@ -72,3 +72,64 @@ def test_value_sampler_matches_reference_counts():
         s = A.ValueSampler(c["rate"])
         vals = [str(v) for v in range(c["n"])] if c["str"] else range(c["n"])
         assert sum(s.keep(v) for v in vals) == c["kept"]
+
+
+@pytest.mark.parametrize("name", ["private_gaussian", "public_gaussian", "private_laplace"])
+def test_oracle_aggregate_matches_reference_golden(name):
+    """pdp_analysis_oracle's perform_utility_analysis restatement against the
+    reference (tests/golden/aggregate_*.npz, oracle/gen_golden.py).  Gaussian
+    quantiles are closed form (exact); Laplace quantiles are the reference's
+    Monte-Carlo estimates, compared by distribution (analysis_util)."""
+    from analysis_util import check_aggregate, oracle_aggregate
+    from golden_util import load
+    d = load("aggregate_" + name)
+    check_aggregate(d, oracle_aggregate(d), rtol=1e-8, atol=1e-9, quantile_sigmas=4.0)
+
+
+def _agg_as_dicts(result):
+    """perform_utility_analysis output -> check_aggregate's per-configuration dicts."""
+    import dataclasses as dc
+    out = []
+    lst = list(result)
+    assert len(lst) == 1
+    for am in lst[0]:
+        d = {"selection": None if am.partition_selection_metrics is None else dc.asdict(am.partition_selection_metrics)}
+        for m in ("count", "privacy_id_count", "sum"):
+            em = getattr(am, m + "_metrics")
+            if em is not None:
+                d[m] = {k: v for k, v in dc.asdict(em).items() if k != "metric_type"}
+        out.append(d)
+    return out
+
+
+def run_perform(name, backend):
+    """pipelinedp_amd.analysis.perform_utility_analysis on an aggregate_* golden."""
+    from golden_util import load
+    d = load("aggregate_" + name)
+    meta = d["meta"]
+    cfg = meta["cfg"]
+    kw = dict(metrics=[{"count": pdp.Metrics.COUNT, "sum": pdp.Metrics.SUM,
+                        "privacy_id_count": pdp.Metrics.PRIVACY_ID_COUNT}[m] for m in cfg["metrics"]],
+              noise_kind=pdp.NoiseKind(cfg["noise_kind"]), max_partitions_contributed=cfg["L0"],
+              max_contributions_per_partition=cfg["Linf"])
+    for k in ("min_sum_per_partition", "max_sum_per_partition"):
+        if cfg.get(k) is not None:
+            kw[k] = cfg[k]
+    multi = A.MultiParameterConfiguration(**meta["multi"]) if meta["multi"] else None
+    options = A.UtilityAnalysisOptions(epsilon=cfg["eps"], delta=cfg["delta"], aggregate_params=pdp.AggregateParams(**kw),
+                                       multi_param_configuration=multi, partitions_sampling_prob=meta["sampling"])
+    rows = list(zip(d["pid"].tolist(), d["pk"].tolist(), d["value"].tolist()))
+    ex = pdp.DataExtractors(privacy_id_extractor=lambda r: r[0], partition_extractor=lambda r: r[1],
+                            value_extractor=lambda r: r[2])
+    public = d["public"].tolist() if bool(d["has_public"]) else None
+    return d, A.perform_utility_analysis(rows, backend, options, ex, public_partitions=public)
+
+
+@pytest.mark.parametrize("name", ["private_gaussian", "public_gaussian", "private_laplace"])
+def test_perform_utility_analysis_host_on_cpu_executor(name):
+    """The host side of perform_utility_analysis (budget split, std_noise, the
+    compute_metrics divisions, AggregateMetrics packing) with the CPU
+    stand-in executor, against the reference goldens."""
+    from analysis_util import check_aggregate
+    d, res = run_perform(name, _backend())
+    check_aggregate(d, _agg_as_dicts(res), rtol=1e-8, atol=1e-9, quantile_sigmas=4.0)
