@@ -111,6 +111,8 @@ __device__ __forceinline__ void st_rec(Rec* p, const Rec& r) {
 #endif
 }
 
+constexpr uint32_t kK4EmptyKey = 0xFFFFFFFFu;  // K4 empty pair slot (pdp_reduce.inc kK4Empty)
+
 struct KeySpec {
   int mode;  // 0: key = pid >> low ; 1: key = (pid << pkb) | pk ; 3: key = (pid, bits(val)) 96-bit ;
              // 4: bucketed pid: passes with shift >= 64 take the bucket digit (pid * mult) >> 32, others pid bits ;
@@ -126,6 +128,7 @@ struct KeySpec {
   uint64_t mult;  // mode 4: bucket digit multiplier (pdp_filter.inc)
   int prof;  // accumulate per-phase s_memtime cycles of k_onesweep (kDebugSweepStamps)
   int ablate;  // kDebugNoLookback / kDebugLinearWrite (timing ablations, results invalid)
+  int64_t cap;  // mode 6: records the output holds; a scatter position beyond it is reported, not written
 };
 
 // How a row's value feeds the accumulators (combiners.py:254-261, 305-311,
@@ -199,10 +202,11 @@ __device__ __forceinline__ uint32_t digit_of(const KeySpec& ks, int pass, const 
   const uint64_t mask = (1ull << ks.bits[pass]) - 1ull;
   const int sh = ks.shift[pass];
   uint64_t key;
-  if (ks.mode == 0) {
-    key = (uint64_t)(r.pid >> ks.low);
-  } else if (ks.mode == 6) {
-    if (r.pid == 0xFFFFFFFFu) return 256u;  // empty slot
+  // Mode 6 (K4 pair records) keys like mode 0; its empty slots are dropped by
+  // the caller (onesweep_body), not here: an extra early-return branch in this
+  // chain was miscompiled on gfx950 (ROCm 7.2) -- the mode 1 / 4 digits of the
+  // survivor and analysis sorts came out wrong (bisected on MI355X).
+  if (ks.mode == 0 || ks.mode == 6) {
     key = (uint64_t)(r.pid >> ks.low);
   } else if (ks.mode == 4) {
     if (sh >= 64) return (uint32_t)(((uint64_t)r.pid * ks.mult) >> 32);
@@ -572,7 +576,7 @@ __device__ __forceinline__ void onesweep_body(
         }
       } else {
         r[k] = idx < split ? ld_rec(rin + idx) : ld_rec(rin2 + (idx - split));
-        d = digit_of(ks, pass, r[k]);
+        d = (ks.mode == 6 && r[k].pid == kK4EmptyKey) ? 256u : digit_of(ks, pass, r[k]);  // K4: empty slot
       }
     }
     dr[k] = d;
@@ -752,6 +756,10 @@ __device__ __forceinline__ void onesweep_body(
         st_rec(rout + tile_start + (long long)(h + i), rc);
       } else {
         const long long q = s_gbase[TAG ? (rc.pid >> 22) & 255u : digit_of(ks, pass, rc)] + (long long)(h + i);
+        if (ks.mode == 6 && (q < 0 || q >= ks.cap)) {  // the pair histogram disagrees with the records
+          atomicOr(&counters[kCtrErr], 4ull);
+          continue;
+        }
         st_rec(rout + q, rc);
         if constexpr (TAG) tag_out[q] = rc.pid;
       }
@@ -2008,13 +2016,14 @@ K4Red k4_red(const K4Plan& k, const SegParams& sp, int64_t P, bool y) {
 int k4_run(pdp_ctx* ctx, hipStream_t stream, const K4Plan& k, const K4Red& kr, bool y, const Rec* in_a,
            int64_t len_a, const Rec* in_b, int64_t len_b, Rec* buf1, Rec* buf2, AccPtrs acc,
            unsigned long long* off, unsigned long long* counters, unsigned long long* status, void* ws,
-           unsigned long long* s_lo, unsigned long long* s_hi, unsigned int* s_fl) {
+           unsigned long long* s_lo, unsigned long long* s_hi, unsigned int* s_fl, int64_t buf_cap) {
   const int64_t total = len_a + len_b;
   if (total == 0) return 0;
   hipLaunchKernelGGL(k4_set_counter, dim3(1), dim3(64), 0, stream, counters, (int)kCtrK4In,
                      (unsigned long long)total);
   KeySpec ks{};
   ks.mode = 6;
+  ks.cap = std::min<int64_t>(total, buf_cap);  // the pairs (< total) land in buf1 / buf2
   ks.low = kr.sh;
   ks.passes = k.passes;
   for (int i = 0; i < k.passes; ++i) {
@@ -2159,11 +2168,11 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
     ctx->stats.k4_slots = nslots + nkf;
     ctx->stats.k4_passes = k4.passes;
     if (int rc = k4_run(ctx, stream, k4, k4_red(k4, q, P, false), false, slots, nslots, kfx, nkf, buf1, buf2, acc, off,
-                        counters, status, workspace, k4lo, k4hi, k4fl))
+                        counters, status, workspace, k4lo, k4hi, k4fl, n))
       return rc;
     if (q.want_y) {
       if (int rc = k4_run(ctx, stream, k4, k4_red(k4, q, P, true), true, k4y, nslots, kfy, nkf, buf1, buf2, acc, off,
-                          counters, status, workspace, k4lo, k4hi, k4fl))
+                          counters, status, workspace, k4lo, k4hi, k4fl, n))
         return rc;
     }
     return 0;
@@ -2436,6 +2445,7 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
     HIP_TRY(hipMemcpyAsync(kc, counters, sizeof(kc), hipMemcpyDeviceToHost, stream));
     HIP_TRY(hipStreamSynchronize(stream));
     ctx->stats.k4_pairs = (int64_t)kc[kCtrK4Pairs];
+    if (kc[kCtrErr] & 4) return fail(PDP_ERR_INTERNAL, "K4 pair histogram disagrees with the pair records");
     if (kc[kCtrErr] & 2) return fail(PDP_ERR_INTERNAL, "K4 pair records not grouped by partition block");
     if (kc[kCtrErr]) return fail(PDP_ERR_INTERNAL, "radix look-back timed out (pair passes)");
   } else if (sp.packed) {
@@ -2894,32 +2904,45 @@ int pdp_utility_aggregate(pdp_ctx* ctx, const double* metrics, const double* pro
   if (!dg.ok) return fail(PDP_ERR_HIP, "hipSetDevice failed");
   hipStream_t stream = (hipStream_t)stream_;
   const int K = kAggFields + 2 * Q;
-  const int nerr = C * nb, nsel = prob_keep ? C : 0, nrows = nerr + nsel;
   const int64_t P = num_partitions;
   // metric blocks in pdp_utility_analysis order: SUM, COUNT, PRIVACY_ID_COUNT (those present)
   int is_sum[3], b = 0;
   for (int m : {PDP_METRIC_SUM, PDP_METRIC_COUNT, PDP_METRIC_PRIVACY_ID_COUNT})
     if (mflags & m) is_sum[b++] = m == PDP_METRIC_SUM;
-  std::vector<AggRow> rows((size_t)nrows);
+  std::vector<AggRow> rows;
   for (int c = 0; c < C; ++c)
     for (int k = 0; k < nb; ++k) {
-      AggRow& r = rows[(size_t)c * nb + k];
+      AggRow r{};
       r.m = metrics + ((size_t)c * nb + k) * 5 * (size_t)P;
       r.prob = prob_keep;  // configuration 0's (combiners.py:470-480)
       r.std_noise = ap->std_noise[(size_t)c * nb + k];
       r.kind = ap->noise_kind[c];
       r.is_sum = is_sum[k];
+      double* base = out_errors + ((size_t)c * nb + k) * K;
+      r.dst = base;
+      r.stride = 1;
+      r.nf = kAggFields;
+      rows.push_back(r);
+      for (int j = 0; j < Q; ++j) {  // error_quantiles[j], rel_error_quantiles[j]
+        r.qrow = 1;
+        r.q = 1.0 - ap->quantiles[j];  // _invert_error_quantiles
+        r.dst = base + kAggFields + j;
+        r.stride = Q;
+        r.nf = 2;
+        rows.push_back(r);
+      }
     }
-  for (int c = 0; c < nsel; ++c) {
-    AggRow& r = rows[(size_t)nerr + c];
-    r.m = nullptr;
-    r.prob = prob_keep + (size_t)c * P;
-  }
+  if (prob_keep)
+    for (int c = 0; c < C; ++c) {
+      AggRow r{};
+      r.prob = prob_keep + (size_t)c * P;
+      r.dst = out_selection + (size_t)c * 3;
+      r.stride = 1;
+      r.nf = 3;
+      rows.push_back(r);
+    }
+  const int nrows = (int)rows.size();
   AggParams prm{};
-  prm.nrows = nrows;
-  prm.K = K;
-  prm.Q = Q;
-  for (int j = 0; j < Q; ++j) prm.q[j] = 1.0 - ap->quantiles[j];  // _invert_error_quantiles
   prm.privacy_ids = privacy_ids;
   prm.P = P;
   const int nblocks = (int)std::max<int64_t>(1, std::min<int64_t>((P + kAggThreads - 1) / kAggThreads, kAggMaxBlocks));
@@ -2927,16 +2950,16 @@ int pdp_utility_aggregate(pdp_ctx* ctx, const double* metrics, const double* pro
   AggRow* d_rows = nullptr;
   double* partials = nullptr;
   HIP_TRY(scratch.alloc((void**)&d_rows, rows.size() * sizeof(AggRow)));
-  HIP_TRY(scratch.alloc((void**)&partials, (size_t)nrows * nblocks * kAggMaxK * sizeof(double)));
+  HIP_TRY(scratch.alloc((void**)&partials, (size_t)nrows * nblocks * kAggFields * sizeof(double)));
   HIP_TRY(hipMemcpyAsync(d_rows, rows.data(), rows.size() * sizeof(AggRow), hipMemcpyHostToDevice, stream));
   prm.rows = d_rows;
   {
     ProfScope ps(ctx, PDP_STAGE_ANALYSIS_AGGREGATE, stream);
     hipLaunchKernelGGL(k_agg_partials, dim3((unsigned)nblocks, (unsigned)nrows), dim3(kAggThreads), 0, stream, prm,
                        partials);
-    const int tot = nrows * kAggMaxK;
-    hipLaunchKernelGGL(k_agg_final, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, stream, partials, nerr, nsel,
-                       nblocks, K, out_errors, out_selection);
+    const int tot = nrows * kAggFields;
+    hipLaunchKernelGGL(k_agg_final, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, stream, partials, d_rows, nrows,
+                       nblocks);
   }
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipStreamSynchronize(stream));  // `rows` (host) is read by the copy above

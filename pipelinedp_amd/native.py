@@ -148,7 +148,11 @@ def lib():
                               "(hipcc --offload-arch=gfx950); there is no CPU fallback.")
         handle = ctypes.CDLL(LIB_PATH)
         for name, res, args in SIGNATURES:
-            fn = getattr(handle, name)
+            fn = getattr(handle, name, None)
+            if fn is None and os.environ.get("PDP_HIP_LIB"):
+                continue  # an experiment build of an older ABI
+            if fn is None:
+                raise NativeError(f"{LIB_PATH} does not export {name}: rebuild it")
             fn.restype = res
             fn.argtypes = args
         _lib = handle

@@ -241,3 +241,50 @@ def test_c5_utility_analysis_full_size(ex):
     assert pr.shape == (len(cfgs), P)
     assert np.all((pr >= 0.0) & (pr <= 1.0 + 1e-12))
     assert np.all(pr[:, distinct.cpu().numpy() == 0] == 0.0)
+
+
+def test_c2_public_partitions_full_size(ex):
+    """c2 (BASELINE configs[1]) at full size: 1e8 rows, 1e6 uniform privacy
+    ids, 2e5 partitions of which the 1e5 even ones are public, so half the rows
+    really drop (_drop_not_public_partitions, dp_engine.py:283-297) before
+    bounding; COUNT + SUM + PRIVACY_ID_COUNT, L0 = 8, Linf = 4, through the L0
+    pre-filter.  Each privacy id keeps min(#public partitions, L0) partitions;
+    per public partition row_count <= count <= min(Linf * row_count, rows);
+    sums of values clipped to [0, 10] lie in [0, 10 * count]; the unfiltered
+    path gives the same counts bit for bit."""
+    import torch
+    from pipelinedp_amd.executor import BoundConfig
+    n, U, P2, L0, Linf, a, b = 100_000_000, 1_000_000, 200_000, 8, 4, 0.0, 10.0
+    pid, pk2, val = ex.generate(n, U, P2, seed=0xC2, zipf_s=0.0, lo=-2.0, hi=12.0)
+    pk = torch.where(pk2 % 2 == 0, pk2 // 2, torch.full_like(pk2, -1))  # public: even keys -> dense ids
+    del pk2
+    P = P2 // 2
+    mask = MASK_COUNT | MASK_SUM | MASK_PID
+    cfg = BoundConfig(mask, L0, Linf, a, b, sampling_seed=21)
+    acc = ex.accumulate(pid, pk, val, U, P, cfg)
+    torch.cuda.synchronize()
+    st = ex.stats()
+    assert st.kept_rows_in == int((pk >= 0).sum())
+    assert 0 < st.filter_rows < st.kept_rows_in  # the pre-filter ran
+    rc, cnt, sm = acc.row_count.clone(), acc.count.clone(), acc.x.clone()
+
+    pub = pk >= 0
+    ppid, ppk = pid[pub], pk[pub]
+    rows_pk = torch.bincount(ppk, minlength=P)
+    keys = _pairs(torch, ppid, ppk, P)
+    del ppid, ppk, pub
+    npk = torch.bincount(keys // P, minlength=U)
+    assert int(rc.sum()) == int(npk.clamp(max=L0).sum())
+    assert bool((rc <= torch.bincount(keys % P, minlength=P)).all())
+    del keys, npk
+    assert bool((cnt >= rc).all())
+    assert bool((cnt <= torch.minimum(Linf * rc, rows_pk)).all())
+    assert bool((sm >= -1e-9).all()) and bool((sm <= b * cnt.to(torch.float64) + 1e-6).all())
+
+    nofilter = BoundConfig(mask, L0, Linf, a, b, sampling_seed=21, debug_flags=NO_FILTER)
+    acc2 = ex.accumulate(pid, pk, val, U, P, nofilter)
+    torch.cuda.synchronize()
+    assert ex.stats().filter_rows == 0
+    assert torch.equal(acc2.row_count, rc)
+    assert torch.equal(acc2.count, cnt)
+    assert bool(((acc2.x - sm).abs() <= 1e-9 * (b * cnt.to(torch.float64) + 1.0)).all())

@@ -14,4 +14,7 @@ for s in "$@"; do
   rc=$?
   echo "   rc=$rc"; tail -n 15 "$O/step$i.log"
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping: step $i rc=$rc"; exit $rc; fi
+  if grep -qi "illegal memory access\|memory access fault\|hipErrorIllegalAddress" "$O/step$i.log"; then
+    echo "stopping: step $i hit a GPU memory fault"; exit 3
+  fi
 done
