@@ -57,13 +57,14 @@ def analysis_oracle_cfgs(eps_sel=0.25, delta_sel=1e-6):
     return [ao.AnalysisConfig(l0, linf, lo, hi, "truncated_geometric", eps_sel, delta_sel) for l0, linf in SWEEP]
 
 
-def pmc_traffic(stage, rows):
-    """HBM bytes per launch of `stage` from profiles/pmc_traffic.json (written by
-    tools/pmc_traffic.py from the separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE
-    passes of tools/profile_round.sh) when that profile was taken on this same
-    workload size; (None, None) otherwise."""
+def pmc_traffic(stage, rows, workload="c3"):
+    """HBM bytes per launch of `stage` from profiles/pmc_traffic[_<workload>].json
+    (written by tools/pmc_traffic.py from the separate rocprofv3 --pmc
+    FETCH_SIZE / WRITE_SIZE passes of tools/profile_round.sh) when that profile
+    was taken on this same workload size; (None, None) otherwise."""
+    name = "pmc_traffic.json" if workload == "c3" else f"pmc_traffic_{workload}.json"
     try:
-        with open(os.path.join(ROOT, "profiles", "pmc_traffic.json")) as f:
+        with open(os.path.join(ROOT, "profiles", name)) as f:
             d = json.load(f)
     except (OSError, ValueError):
         return None, None
@@ -413,7 +414,7 @@ def main():
         nb = (P + world_size - 1) // world_size if world else P
         b = stage_bytes(dom, n, rows_after_public_filter, nb, len(fields), surv, surv_passes, k4)
         ach = b / (stages[dom]["ms_per_launch"] * 1e-3) / 1e9
-        traffic, prof_round = pmc_traffic(dom, n) if not sweep else (None, None)
+        traffic, prof_round = pmc_traffic(dom, n, args.workload) if not sweep else (None, None)
         roofline = {"bound": "hbm", "kernel": dom, "achieved": round(ach, 1), "peak": PEAK_HBM_GBS,
                     "unit": "GB/s", "frac": round(ach / PEAK_HBM_GBS, 4), "traffic": None,
                     "traffic_note": "HBM bytes need separate rocprofv3 --pmc passes (FETCH_SIZE x2 on gfx950 + "
