@@ -1495,6 +1495,8 @@ struct ProfScope {
   }
 };
 
+int env_int(const char* name, int def);
+
 int next_epoch(pdp_ctx* ctx, hipStream_t stream, unsigned long long* status, size_t status_bytes, void* ws) {
   if (ctx->last_ws != ws || ctx->epoch >= 0xFFFE || status_bytes > ctx->status_ok) {
     HIP_TRY(hipMemsetAsync(status, 0, status_bytes, stream));
@@ -1575,7 +1577,7 @@ int sort_recs(pdp_ctx* ctx, Rec* a, Rec* b, int64_t m, const KeySpec& ks, unsign
   Rec* src = a;
   Rec* dst = b;
   const int64_t tiles = (m + kTile - 1) / kTile;
-  const bool rts = use_tile_scan(m, 0);
+  const bool rts = use_tile_scan(m, 0) && !env_int("PDP_SORT_LOOKBACK", 0);
   for (int p = 0; p < ks.passes; ++p) {
     const unsigned int* bases = nullptr;
     if (rts) {
@@ -1956,6 +1958,7 @@ FilterPlan filter_plan(int64_t n, int64_t U, const pdp_bound_params* bp, int deb
 // accumulators then take fp64 atomics, as in round 2.
 struct K4Plan {
   bool on;
+  int sh;  // partition block = pk >> sh (LDS window of the reduction: 2^sh partitions)
   int passes;
   int shift[kK4MaxPasses], bits[kK4MaxPasses];
   int fx, fy;  // fixed-point exponents: q = rint(x * 2^f)
@@ -1976,7 +1979,11 @@ K4Plan k4_plan(const pdp_bound_params* bp, const SegParams& sp, int64_t n, int64
   k.on = k4_enabled(n, sweep);
   if (!k.on) return k;
   const int pkb = std::max(1, pdp::ceil_log2_u64((uint64_t)std::max<int64_t>(P, 1)));
-  const int kb = std::max(1, pkb - kK4Sh);
+  // the 2048-partition window (56 KiB of LDS: 2 reduce workgroups per CU) unless the 4096 one saves a pass
+  auto npasses = [&](int sh) { return (std::max(1, pkb - sh) + 7) / 8; };
+  k.sh = npasses(kK4ShMax) < npasses(kK4ShMax - 1) ? kK4ShMax : kK4ShMax - 1;
+  if (const int e = env_int("PDP_K4_SH", 0)) k.sh = std::min(kK4ShMax, std::max(kK4ShMax - 1, e));
+  const int kb = std::max(1, pkb - k.sh);
   k.passes = (kb + 7) / 8;
   int rem = kb, sh = 0;
   for (int i = 0; i < k.passes; ++i) {
@@ -2001,13 +2008,14 @@ K4Plan k4_plan(const pdp_bound_params* bp, const SegParams& sp, int64_t n, int64
 K4Red k4_red(const K4Plan& k, const SegParams& sp, int64_t P, bool y) {
   K4Red r{};
   const int f = y ? k.fy : k.fx;
-  r.sh = kK4Sh;
+  r.sh = k.sh;
   r.want_count = sp.want_count;
   r.want_x = sp.xmode != kXNone;
   r.P = P;
   r.q = std::ldexp(1.0, f);
   r.inv_hi = std::ldexp(1.0, 32 - f);
   r.inv_lo = std::ldexp(1.0, -f);
+  r.chunk = std::max(4096, env_int("PDP_K4_CHUNK", (int)kK4Chunk));
   return r;
 }
 
@@ -2054,17 +2062,15 @@ int k4_run(pdp_ctx* ctx, hipStream_t stream, const K4Plan& k, const K4Red& kr, b
   }
   HIP_TRY(hipGetLastError());
   ProfScope ps(ctx, PDP_STAGE_REDUCE, stream);
-  const int64_t chunks = (total + kK4Chunk - 1) / kK4Chunk;
+  const int64_t chunks = (total + kr.chunk - 1) / kr.chunk;
   const bool scratch = (y || kr.want_x) && chunks > 1;
   if (scratch)
     hipLaunchKernelGGL(k4_zero_shared, dim3((unsigned)(chunks - 1)), dim3(kThreads), 0, stream, src, counters, kr.sh,
-                       kr.P, s_lo, s_hi, s_fl);
-  if (y)
-    hipLaunchKernelGGL(k4_reduce<true>, dim3((unsigned)chunks), dim3(kK4Threads), 0, stream, src, counters, kr, acc,
-                       s_lo, s_hi, s_fl);
-  else
-    hipLaunchKernelGGL(k4_reduce<false>, dim3((unsigned)chunks), dim3(kK4Threads), 0, stream, src, counters, kr, acc,
-                       s_lo, s_hi, s_fl);
+                       kr.P, kr.chunk, s_lo, s_hi, s_fl);
+  auto kern = y ? (kr.sh == kK4ShMax ? k4_reduce<true, kK4ShMax> : k4_reduce<true, kK4ShMax - 1>)
+               : (kr.sh == kK4ShMax ? k4_reduce<false, kK4ShMax> : k4_reduce<false, kK4ShMax - 1>);
+  hipLaunchKernelGGL(kern, dim3((unsigned)chunks), dim3(kK4Threads), 0, stream, src, counters, kr, acc, s_lo, s_hi,
+                     s_fl);
   if (scratch) {
     if (y)
       hipLaunchKernelGGL(k4_finalize<true>, dim3((unsigned)(chunks - 1)), dim3(kThreads), 0, stream, src, counters,
@@ -2154,7 +2160,7 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
     q.k4x = slots;
     q.k4y = k4y;
     q.k4hist = k4rep;
-    q.k4sh = kK4Sh;
+    q.k4sh = k4.sh;
     q.k4passes = k4.passes;
     for (int i = 0; i < kK4MaxPasses; ++i) {
       q.k4shift[i] = k4.shift[i];
@@ -2244,9 +2250,13 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
                      (int)kCtrNKept);
   Rec* src = nullptr;
   Rec* dst = recs_a;
+  // Passes >= 1 by decoupled look-back: at c4 (3 passes) the look-back passes took 12.28 ms for
+  // two against 10.7 + 3.22 ms with the reduce-then-scan upsweeps (same box).  Pass 0 keeps the
+  // tile counts K0 produces anyway.
+  const bool rest_tile_scan = env_int("PDP_PASS_TILESCAN", 0) != 0;
   for (int p = 0; p < ks.passes; ++p) {
     const unsigned int* bases = nullptr;
-    if (rts) {
+    if (rts && (p == 0 || rest_tile_scan)) {
       ProfScope ps(ctx, PDP_STAGE_TILE_COUNTS, stream);
       if (p > 0)
         hipLaunchKernelGGL(k_tile_counts, dim3(grid_for(L.tiles, 1, 4096)), dim3(kThreads), 0, stream, src, counters,
