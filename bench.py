@@ -117,10 +117,8 @@ def stage_bytes(stage, n_in, n_kept, P, nfields, survivors=0, survivor_passes=0,
         "onesweep_first": (24 + 16 + (4 if survivors else 0)) * n_in,  # read 3 columns, write 16-B records (+ tags)
         "onesweep_rest": 32 * n_kept,  # read + write 16-B records
         "filter": 12 * n_kept + 32 * survivors,  # tags three times, survivors' records read + written
-        # k_group_survivors (no radix pass): the survivors read twice (count, place) + written once;
-        # survivor radix sort: histogram read + per pass (read + write) + per later pass an upsweep read
-        "survivor_sort": survivors * (48 if survivor_passes == 0 else
-                                      16 + 32 * survivor_passes + 16 * max(survivor_passes - 1, 0)),
+        # histogram read + per pass (read + write) + per later pass an upsweep read
+        "survivor_sort": survivors * (16 + 32 * survivor_passes + 16 * max(survivor_passes - 1, 0)),
         "buckets": 16 * sorted_rows + 16 * slots,  # read 16-B records once (+ K4: write the pair slots)
         "pair_pass": 16 * slots + 16 * pairs + 32 * pairs * max(kpasses - 1, 0),
         "reduce": 16 * pairs + 24 * P,

@@ -1320,7 +1320,7 @@ int grid_for(int64_t n, int threads, int cap = 4096) {
 }
 
 struct Layout {
-  size_t recs_a, recs_b, recs_c, hist, off, counters, status, ranges, big, tags, tag_lo, keep, runs, k4rep, k4s, total;
+  size_t recs_a, recs_b, recs_c, hist, off, counters, status, ranges, big, tags, tag_lo, keep, k4rep, k4s, total;
   int64_t tiles;
   uint64_t big_cap;
 };
@@ -1347,7 +1347,6 @@ Layout layout_for(int64_t n, bool sweep = false, int64_t k4p = 0, bool variance 
   L.tags = o; o += sweep ? 0 : align_up((size_t)std::max<int64_t>(n, 1) * 4, 256);  // L0 pre-filter tags
   L.tag_lo = o; o += 256 * 4;
   L.keep = o; o += sweep ? 0 : align_up((size_t)std::max<int64_t>(n, 1) / 4 + 64, 256);  // k_filter keep bytes
-  L.runs = o; o += sweep ? 0 : 256 * 16;  // k_filter's survivor run per bucket (k_group_survivors)
   L.k4rep = o; o += k4p > 0 ? align_up((size_t)kK4Rep * kK4MaxPasses * 256 * 4, 256) : 0;
   L.k4s = o; o += k4p > 0 ? align_up((size_t)k4p * 20, 256) : 0;
   L.total = o;
@@ -2302,18 +2301,13 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
   if (fpl.on) {
     // K1f: survivors of the bucket-sorted rows -> spare (input order per pid kept)
     HIP_TRY(hipMemsetAsync(counters + kCtrNSurv, 0, 8, stream));
-    // survivors grouped by pid in each bucket's run (k_group_survivors) instead of the survivor radix
-    // sort: buckets of <= kFiltWords pids (not HALF); PDP_SURVIVOR_SORT=1 keeps the sort (A/B)
-    const bool group = !fpl.half && env_int("PDP_SURVIVOR_SORT", 0) == 0;
-    unsigned long long* runs = group ? (unsigned long long*)(ws + L.runs) : nullptr;
-    if (group) HIP_TRY(hipMemsetAsync(runs, 0, 256 * 16, stream));
     {
       ProfScope ps(ctx, PDP_STAGE_FILTER, stream);
       hipLaunchKernelGGL(fpl.half ? k_filter<true> : k_filter<false>, dim3(256), dim3(kFiltThreads), 0, stream,
                          sorted, tags, tag_lo, spare,
                          (uint8_t*)(ws + L.keep), off, counters,
                          (int)kCtrNKept, (int)kCtrNSurv, (int)bp->max_partitions_contributed,
-                         (sp.debug & kDebugFilterTiming) != 0, runs);
+                         (sp.debug & kDebugFilterTiming) != 0);
     }
     HIP_TRY(hipGetLastError());
     unsigned long long m = 0;
@@ -2325,16 +2319,6 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
     // from different buckets stay in the order of their buckets' runs, because k_filter writes each
     // bucket's survivors as ONE contiguous run.  (No bucket-digit pass: the order of the pids does
     // not matter to K2, only their grouping.)
-    if (group) {
-      {
-        ProfScope ps(ctx, PDP_STAGE_SURVIVOR_SORT, stream);
-        hipLaunchKernelGGL(k_group_survivors, dim3(256), dim3(kFiltThreads), 0, stream, spare, sorted, runs, tag_lo,
-                           counters);
-      }
-      HIP_TRY(hipGetLastError());
-      n_slot = kCtrNSurv;  // the grouped survivors are in `sorted`; `spare` (k_filter's output) is free
-      n_sorted = m;
-    } else {
     KeySpec k2 = ks;
     k2.passes = 0;
     for (int sh = 0; sh < fpl.low_bits; sh += 8) {
@@ -2354,7 +2338,6 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
     spare = (out == sa) ? sb : sa;
     n_slot = kCtrNGeneric;
     n_sorted = m;
-    }
   }
 
   OvList ov{ranges, counters};
@@ -2428,7 +2411,6 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
   n_kept = host_ctr[n_slot];
   for (int i = 0; i < 4; ++i) ctx->stats.sweep_cycles[i] = (int64_t)host_ctr[kCtrSweepCycles + i];
   ctx->stats.sweep_tiles = (int64_t)host_ctr[kCtrSweepTiles];
-  if (host_ctr[kCtrErr] & 8) return fail(PDP_ERR_INTERNAL, "survivor grouping: wave turn timed out");
   if (host_ctr[kCtrErr]) return fail(PDP_ERR_INTERNAL, "radix look-back timed out");
   if (host_ctr[kCtrInvalid]) return fail(PDP_ERR_OUT_OF_RANGE, "privacy id or partition id out of range");
   std::vector<unsigned long long> rg;
