@@ -183,6 +183,7 @@ constexpr int kDebugNoFilter = 134217728;      // never use the L0 pre-filter (p
 constexpr int kDebugForceFilter = 268435456;   // use the L0 pre-filter whenever it applies (small inputs too)
 constexpr int kDebugNoThin = 536870912;        // bound the pre-filter's survivors with k_lean instead of k_thin
 constexpr int kDebugFilterTiming = 1073741824;  // k_filter timing ablation: phase 1 only (results invalid)
+constexpr int kDebugLinfSort = 1 << 22;  // lean_segment_sorted: L_inf by a second wave sort (round-2 form)
 
 struct AccPtrs {
   unsigned long long* row_count;
