@@ -48,6 +48,11 @@ WORKLOADS = {
 }
 SWEEP = [(l0, linf) for l0 in (1, 2, 4, 8, 16, 32, 64, 128) for linf in range(1, 9)]
 SWEEP_SUM_BOUNDS = (0.0, 20.0)  # min/max_sum_per_partition of every c5 configuration
+# fp64 operations k_ana_metrics spends per (pair, configuration) with SUM + COUNT + PRIVACY_ID_COUNT
+# (pdp_analysis.inc): q 1, q(1-q) 2, SumCombiner terms 11, CountCombiner 10,
+# PrivacyIdCountCombiner 4, selection moments 7
+ANALYSIS_FLOP_PER_PAIR_CONFIG = 35
+FP64_SPEC_TFLOPS = 78.6  # MI355X fp64 vector peak (AMD spec; MI355X_MICROARCH.md lists none)
 
 
 def analysis_oracle_cfgs(eps_sel=0.25, delta_sel=1e-6):
@@ -410,6 +415,11 @@ def main():
         for s, (ms, cnt) in prof.items():
             if cnt:
                 stages[s] = {"ms_per_launch": ms / cnt, "launches_per_step": cnt / args.steps}
+        if sweep and "analysis_select" in stages and "analysis_metrics" in stages:
+            # the select launches run inside the metrics stage: report k_ana_metrics on its own
+            m, sel = stages["analysis_metrics"], stages["analysis_select"]
+            m["ms_per_launch"] = (m["ms_per_launch"] * m["launches_per_step"] -
+                                  sel["ms_per_launch"] * sel["launches_per_step"]) / m["launches_per_step"]
         dom = max(stages, key=lambda s: stages[s]["ms_per_launch"] * stages[s]["launches_per_step"])
         nb = (P + world_size - 1) // world_size if world else P
         b = stage_bytes(dom, n, rows_after_public_filter, nb, len(fields), surv, surv_passes, k4)
@@ -428,6 +438,25 @@ def main():
                                       "Poisson-binomial pmf per partition); the HBM fraction is reported for "
                                       "completeness only"} if sweep else {}),
                     "ms_per_launch_source": "hipEvents on the launch stream, averaged over the timed steps"}
+        if sweep:
+            # fp64-VALU bound: FLOP/s of k_ana_metrics against the box's measured fp64 FMA rate
+            import ctypes
+            tf = ctypes.c_double(0.0)
+            native.check(native.lib().pdp_fp64_probe(ctypes.byref(tf), ex.stream_handle), "pdp_fp64_probe")
+            flops = rows_after_public_filter * len(SWEEP) * ANALYSIS_FLOP_PER_PAIR_CONFIG
+            ms = stages["analysis_metrics"]["ms_per_launch"]
+            ach = flops / (ms * 1e-3) / 1e12
+            roofline = {"bound": "fp64", "kernel": "analysis_metrics (k_ana_metrics)", "achieved": round(ach, 2),
+                        "peak": round(tf.value, 1), "unit": "TFLOP/s", "frac": round(ach / tf.value, 4),
+                        "peak_note": "pdp_fp64_probe: fp64 FMA chains on this box (2 FLOP per FMA); AMD spec "
+                                     f"{FP64_SPEC_TFLOPS} TFLOP/s",
+                        "frac_of_spec": round(ach / FP64_SPEC_TFLOPS, 4),
+                        "algorithmic_flops_per_launch": flops,
+                        "flops_note": f"{ANALYSIS_FLOP_PER_PAIR_CONFIG} fp64 operations per (pair, configuration) "
+                                      f"x {rows_after_public_filter} pairs x {len(SWEEP)} configurations",
+                        "traffic": None,
+                        "ms_per_launch_source": "hipEvents on the launch stream (analysis_metrics minus the nested "
+                                                "analysis_select), averaged over the timed steps"}
         for s in stages:
             bs = stage_bytes(s, n, rows_after_public_filter, nb, len(fields), surv, surv_passes, k4)
             if bs:

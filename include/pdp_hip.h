@@ -351,6 +351,11 @@ int pdp_generate_synthetic(int64_t* pid, int64_t* pk, double* value, int64_t n, 
  * counterpart; measurement only). */
 int pdp_stream_copy(const void* src, void* dst, int64_t bytes, void* stream);
 
+/* fp64 FMA-chain probe: the device's achievable fp64 vector rate in TFLOP/s
+ * (2 FLOP per FMA), timed with hipEvents on `stream` (synchronises).
+ * Measurement only: the denominator of the utility analysis' roofline. */
+int pdp_fp64_probe(double* tflops, void* stream);
+
 /* Statistics of the last pdp_bound_accumulate on this ctx (host values). */
 typedef struct pdp_stats {
   int64_t kept_rows_in;        /* rows after dropping non-public partitions */
@@ -387,7 +392,8 @@ enum {
   PDP_STAGE_REDUCE = 13,        /* K4 per-partition fixed-point reduction (+ shared-block zero / finalize) */
   PDP_STAGE_ANALYSIS_SORT = 14, /* utility analysis: the (pk, pid) radix sort inside ANALYSIS_PAIRS */
   PDP_STAGE_ANALYSIS_AGGREGATE = 15, /* utility analysis: cross-partition aggregate error metrics */
-  PDP_NUM_STAGES = 16,
+  PDP_STAGE_ANALYSIS_SELECT = 16, /* utility analysis: Poisson-binomial keep probability (inside ANALYSIS_METRICS) */
+  PDP_NUM_STAGES = 17,
 };
 int pdp_profile_enable(pdp_ctx* ctx, int enable);
 /* Waits for recorded events; adds into ms_out/launches_out[PDP_NUM_STAGES]

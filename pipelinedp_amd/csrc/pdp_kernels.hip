@@ -1250,6 +1250,37 @@ __global__ __launch_bounds__(256) void k_stream_copy(const u32x4* __restrict__ s
   for (; i < n16; i += stride) dst[i] = src[i];
 }
 
+// fp64 FMA chains (pdp_fp64_probe): 8 independent chains per lane, no memory traffic but one store.
+__global__ __launch_bounds__(256) void k_fp64_probe(double* __restrict__ out, int iters, double a, double b) {
+  double v[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) v[k] = (double)(threadIdx.x + k) * 1e-3;
+  for (int it = 0; it < iters; ++it) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = fma(v[k], a, b);
+  }
+  double s = 0.0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) s += v[k];
+  if (s == 12345.678) out[blockIdx.x] = s;  // keeps the chains alive
+}
+
+// Variant: 8 loads in flight per lane, non-temporal loads and stores (streaming data that is never
+// re-read should not displace L2 / Infinity-Cache lines).
+__global__ __launch_bounds__(256) void k_stream_copy_nt(const u32x4* __restrict__ src, u32x4* __restrict__ dst,
+                                                        int64_t n16) {
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  for (; i + 7 * stride < n16; i += 8 * stride) {
+    u32x4 v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = __builtin_nontemporal_load(src + i + k * stride);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) __builtin_nontemporal_store(v[k], dst + i + k * stride);
+  }
+  for (; i < n16; i += stride) dst[i] = src[i];
+}
+
 // ---------------------------------------------------------------------------
 // Synthetic generator (oracle/pdp_oracle.py:synth_rows)
 // ---------------------------------------------------------------------------
@@ -2691,6 +2722,7 @@ int analysis_impl(pdp_ctx* ctx, const int64_t* pid, const int64_t* pk, const dou
                        pcnt, psum, npart, M, cfg_d, nconf, mflags, P, out->metrics, mom);
   }
   if (priv) {
+    ProfScope ps_sel(ctx, PDP_STAGE_ANALYSIS_SELECT, stream);
     const int64_t blocks = std::min<int64_t>((P + kAnaSelWaves - 1) / kAnaSelWaves, 16384);
     hipLaunchKernelGGL(k_ana_select<true>, dim3((unsigned)blocks, cgroups), dim3(64 * kAnaSelWaves), 0, stream, pref,
                        npart, pbeg, P, cfg_d, nconf, (const double*)mom, out->prob_keep);
@@ -3061,11 +3093,43 @@ int pdp_generate_synthetic(int64_t* pid, int64_t* pk, double* value, int64_t n, 
   return 0;
 }
 
+int pdp_fp64_probe(double* tflops, void* stream_) {
+  if (!tflops) return fail(PDP_ERR_INVALID_ARG, "null argument");
+  hipStream_t stream = (hipStream_t)stream_;
+  const int blocks = 256 * 16, iters = 4096;
+  double* out = nullptr;
+  HIP_TRY(hipMallocAsync((void**)&out, blocks * sizeof(double), stream));
+  hipLaunchKernelGGL(k_fp64_probe, dim3(blocks), dim3(256), 0, stream, out, iters, 0.999999, 1e-7);  // warm-up
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  HIP_TRY(hipEventCreate(&e0));
+  HIP_TRY(hipEventCreate(&e1));
+  HIP_TRY(hipEventRecord(e0, stream));
+  hipLaunchKernelGGL(k_fp64_probe, dim3(blocks), dim3(256), 0, stream, out, iters, 0.999999, 1e-7);
+  HIP_TRY(hipEventRecord(e1, stream));
+  HIP_TRY(hipEventSynchronize(e1));
+  float ms = 0.f;
+  HIP_TRY(hipEventElapsedTime(&ms, e0, e1));
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  HIP_TRY(hipFreeAsync(out, stream));
+  HIP_TRY(hipStreamSynchronize(stream));
+  *tflops = 2.0 * 8.0 * iters * (double)blocks * 256.0 / (ms * 1e-3) / 1e12;
+  return 0;
+}
+
 int pdp_stream_copy(const void* src, void* dst, int64_t bytes, void* stream) {
   if (bytes < 0 || (bytes & 15) || (bytes && (!src || !dst))) return fail(PDP_ERR_INVALID_ARG, "bad copy args");
   if (bytes == 0) return 0;
-  hipLaunchKernelGGL(k_stream_copy, dim3(8192), dim3(256), 0, (hipStream_t)stream, (const u32x4*)src, (u32x4*)dst,
-                     bytes / 16);
+  // default: non-temporal, 8 x 16 B in flight per lane, 32768 blocks (5.32 TB/s against 5.11 for the plain
+  // 4-deep form on the same box, tools/copy_probe.py)
+  const int variant = env_int("PDP_COPY_VARIANT", 1);
+  const unsigned grid = (unsigned)env_int("PDP_COPY_GRID", 32768);
+  if (variant == 1)
+    hipLaunchKernelGGL(k_stream_copy_nt, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const u32x4*)src,
+                       (u32x4*)dst, bytes / 16);
+  else
+    hipLaunchKernelGGL(k_stream_copy, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const u32x4*)src, (u32x4*)dst,
+                       bytes / 16);
   HIP_TRY(hipGetLastError());
   return 0;
 }

@@ -123,6 +123,7 @@ SIGNATURES = [
     ("pdp_generate_synthetic", c_i32, [c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_f64, c_i32, c_f64,
                                        c_f64, c_u64, c_vp]),
     ("pdp_stream_copy", c_i32, [c_vp, c_vp, c_i64, c_vp]),
+    ("pdp_fp64_probe", c_i32, [ctypes.POINTER(c_f64), c_vp]),
     ("pdp_get_stats", c_i32, [c_vp, ctypes.POINTER(Stats)]),
     ("pdp_profile_enable", c_i32, [c_vp, c_i32]),
     ("pdp_profile_read", c_i32, [c_vp, ctypes.POINTER(c_f64), ctypes.POINTER(c_i64), c_i32]),
@@ -130,7 +131,7 @@ SIGNATURES = [
 
 STAGES = ["histogram", "onesweep_first", "onesweep_rest", "buckets", "generic", "release", "enforced",
           "tile_counts", "analysis_pairs", "analysis_metrics", "filter", "survivor_sort", "pair_pass", "reduce",
-          "analysis_sort", "analysis_aggregate"]
+          "analysis_sort", "analysis_aggregate", "analysis_select"]
 
 _lib = None
 
