@@ -474,8 +474,9 @@ def main():
     copy_gbs = copy_peak_gbs(torch, native.lib()) if rank == 0 and not args.no_profile else None
     if roofline is not None:
         roofline["copy_peak_measured"] = copy_gbs
-        roofline["copy_peak_note"] = ("pdp_stream_copy: 16-B-per-lane streaming copy of 8 GiB, (read + write) bytes / "
-                                      "time; the achievable ceiling next to the 8 TB/s spec peak")
+        roofline["copy_peak_note"] = ("pdp_stream_copy: non-temporal 16-B-per-lane streaming copy of 8 GiB (8 loads "
+                                      "in flight per lane), (read + write) bytes / time; the achievable ceiling next "
+                                      "to the 8 TB/s spec peak")
     if rank == 0:
         e2e = rows_per_s * 24 / 1e9
         line = {
