@@ -128,6 +128,7 @@ struct KeySpec {
   uint64_t mult;  // mode 4: bucket digit multiplier (pdp_filter.inc)
   int prof;  // accumulate per-phase s_memtime cycles of k_onesweep (kDebugSweepStamps)
   int ablate;  // kDebugNoLookback / kDebugLinearWrite (timing ablations, results invalid)
+  int xcd_remap;  // reduce-then-scan passes: blocks sharing an XCD take one contiguous run of tiles
   int64_t cap;  // mode 6: records the output holds; a scatter position beyond it is reported, not written
 };
 
@@ -298,6 +299,11 @@ __device__ __forceinline__ T block_max(T v, T* s_tmp) {
 // K0: digit histograms of every pass from one read of the keys
 // ---------------------------------------------------------------------------
 
+#ifndef PDP_HIST_UNROLL
+#define PDP_HIST_UNROLL 8
+#endif
+constexpr int kHistUnroll = PDP_HIST_UNROLL;  // rows per thread with loads in flight together (K0, K1u)
+
 template <bool SOA>
 __global__ __launch_bounds__(kThreads) void k_histogram(const int64_t* __restrict__ pid,
                                                         const int64_t* __restrict__ pk,
@@ -308,23 +314,37 @@ __global__ __launch_bounds__(kThreads) void k_histogram(const int64_t* __restric
   for (int i = threadIdx.x; i < kMaxPasses * kHist; i += kThreads) sh[i] = 0;
   __syncthreads();
   unsigned int invalid = 0;
-  const int64_t stride = (int64_t)gridDim.x * kThreads;
-  for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < n; i += stride) {
-    Rec r;
-    if (SOA) {
-      const int64_t a = pid[i], b = pk[i];
-      if (b < 0 || b >= (int64_t)ks.num_parts || a < 0 || a >= (int64_t)ks.num_pids) {
-        if (b >= 0) ++invalid;
-        atomicAdd(&sh[256], 1u);
-        continue;
+  // kHistUnroll rows per thread per step, loads first (clamped indices), so
+  // they are in flight together instead of one HBM round trip per row.
+  const int64_t stride = (int64_t)gridDim.x * kThreads * kHistUnroll;
+  for (int64_t i0 = (int64_t)blockIdx.x * kThreads * kHistUnroll + threadIdx.x; i0 < n; i0 += stride) {
+    Rec r[kHistUnroll];
+    int64_t a[kHistUnroll], b[kHistUnroll];
+#pragma unroll
+    for (int u = 0; u < kHistUnroll; ++u) {
+      const int64_t i = i0 + (int64_t)u * kThreads, ic = i < n ? i : n - 1;
+      if (SOA) {
+        a[u] = pid[ic];
+        b[u] = pk[ic];
+      } else {
+        r[u] = rin[ic];
       }
-      r.pid = (uint32_t)a;
-      r.pk = (uint32_t)b;
-      r.val = 0.0;
-    } else {
-      r = rin[i];
     }
-    for (int p = 0; p < ks.passes; ++p) atomicAdd(&sh[p * kHist + digit_of(ks, p, r)], 1u);
+#pragma unroll
+    for (int u = 0; u < kHistUnroll; ++u) {
+      if (i0 + (int64_t)u * kThreads >= n) break;
+      if (SOA) {
+        if (b[u] < 0 || b[u] >= (int64_t)ks.num_parts || a[u] < 0 || a[u] >= (int64_t)ks.num_pids) {
+          if (b[u] >= 0) ++invalid;
+          atomicAdd(&sh[256], 1u);
+          continue;
+        }
+        r[u].pid = (uint32_t)a[u];
+        r[u].pk = (uint32_t)b[u];
+        r[u].val = 0.0;
+      }
+      for (int p = 0; p < ks.passes; ++p) atomicAdd(&sh[p * kHist + digit_of(ks, p, r[u])], 1u);
+    }
   }
   __syncthreads();
   for (int i = threadIdx.x; i < ks.passes * kHist; i += kThreads)
@@ -355,25 +375,33 @@ __global__ __launch_bounds__(kThreads) void k_histogram_tiles(const int64_t* __r
   const int64_t tiles = (n + kTile - 1) / kTile;
   for (int64_t tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
     const int64_t base = tile * kTile + t;
-#pragma unroll 4
-    for (int k = 0; k < kItems; ++k) {
-      const int64_t i = base + (int64_t)k * kThreads;
-      if (i >= n) break;
-      const int64_t a = pid[i];
-      const int64_t b = PID_ONLY ? 0 : pk[i];
-      if (b < 0 || b >= (int64_t)ks.num_parts || a < 0 || a >= (int64_t)ks.num_pids) {
-        if (b >= 0) ++invalid;
-        atomicAdd(&sh[256], 1u);
-        continue;
+    const bool full = (tile + 1) * kTile <= n;
+#pragma unroll
+    for (int g = 0; g < kItems; g += kHistUnroll) {
+      int64_t a[kHistUnroll], b[kHistUnroll];
+#pragma unroll
+      for (int u = 0; u < kHistUnroll; ++u) {  // loads first (clamped), then the counting
+        const int64_t i = base + (int64_t)(g + u) * kThreads, ic = full || i < n ? i : n - 1;
+        a[u] = pid[ic];
+        b[u] = PID_ONLY ? 0 : pk[ic];
       }
-      Rec r;
-      r.pid = (uint32_t)a;
-      r.pk = (uint32_t)b;
-      r.val = 0.0;
-      const uint32_t d0 = digit_of(ks, 0, r);
-      atomicAdd(&sh[d0], 1u);
-      atomicAdd(&st[d0], 1u);
-      for (int p = 1; p < ks.passes; ++p) atomicAdd(&sh[p * kHist + digit_of(ks, p, r)], 1u);
+#pragma unroll
+      for (int u = 0; u < kHistUnroll; ++u) {
+        if (!full && base + (int64_t)(g + u) * kThreads >= n) break;
+        if (b[u] < 0 || b[u] >= (int64_t)ks.num_parts || a[u] < 0 || a[u] >= (int64_t)ks.num_pids) {
+          if (b[u] >= 0) ++invalid;
+          atomicAdd(&sh[256], 1u);
+          continue;
+        }
+        Rec r;
+        r.pid = (uint32_t)a[u];
+        r.pk = (uint32_t)b[u];
+        r.val = 0.0;
+        const uint32_t d0 = digit_of(ks, 0, r);
+        atomicAdd(&sh[d0], 1u);
+        atomicAdd(&st[d0], 1u);
+        for (int p = 1; p < ks.passes; ++p) atomicAdd(&sh[p * kHist + digit_of(ks, p, r)], 1u);
+      }
     }
     __syncthreads();
     tile_cnt[tile * 256 + t] = st[t];
@@ -401,10 +429,17 @@ __global__ __launch_bounds__(kThreads) void k_tile_counts(const Rec* __restrict_
   const int64_t n = (int64_t)counters_n[n_slot];
   for (int64_t tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
     const int64_t base = tile * kTile + t;
-#pragma unroll 4
-    for (int k = 0; k < kItems; ++k) {
-      const int64_t i = base + (int64_t)k * kThreads;
-      if (i < n) atomicAdd(&st[digit_of(ks, pass, rin[i])], 1u);
+#pragma unroll
+    for (int g = 0; g < kItems; g += kHistUnroll) {
+      Rec r[kHistUnroll];
+#pragma unroll
+      for (int u = 0; u < kHistUnroll; ++u) {
+        const int64_t i = base + (int64_t)(g + u) * kThreads;
+        r[u] = rin[i < n ? i : n - 1];
+      }
+#pragma unroll
+      for (int u = 0; u < kHistUnroll; ++u)
+        if (base + (int64_t)(g + u) * kThreads < n) atomicAdd(&st[digit_of(ks, pass, r[u])], 1u);
     }
     __syncthreads();
     tile_cnt[tile * 256 + t] = st[t];
@@ -496,6 +531,14 @@ constexpr int kLookback = PDP_LOOKBACK;
 // per-tile latency chain (tile claim, loads, look-back) is hidden by the
 // other blocks instead of idling the CU.
 constexpr int kHalfTile = kTile / PDP_OS_STAGE_DIV;
+#ifndef PDP_SOA_GROUP
+#define PDP_SOA_GROUP 1
+#endif
+constexpr int kSoaGroup = PDP_SOA_GROUP;  // SoA rows loaded per batch (first pass / bucket pass)
+#ifndef PDP_REC_GROUP
+#define PDP_REC_GROUP 16
+#endif
+constexpr int kRecGroup = PDP_REC_GROUP;  // records loaded per batch (passes on records)
 constexpr uint32_t kNoPos = 0xFFFFu;
 
 // TAG (the bucket pass of the L0 pre-filter, pdp_filter.inc): also writes,
@@ -507,6 +550,13 @@ constexpr uint32_t kNoPos = 0xFFFFu;
 // lane to scratch: ~8 GB of extra traffic per 1e9 rows).
 // rin2 / split (K4 pair passes): input record i is rin[i] for i < split, else rin2[i - split] (the
 // first pair pass reads K2's slots followed by the generic path's pairs).
+// Bijective XCD swizzle (cdna_hip_programming.md T1): blocks b with equal
+// b % 8 get one contiguous range of ids, in dispatch order.
+__device__ __forceinline__ uint32_t xcd_tile(uint32_t b, uint32_t nwg) {
+  const uint32_t q = nwg / 8u, r = nwg % 8u, x = b % 8u;
+  return (x < r ? x * (q + 1u) : r * (q + 1u) + (x - r) * q) + b / 8u;
+}
+
 template <bool SOA, bool TAG = false>
 __device__ __forceinline__ void onesweep_body(
     const int64_t* __restrict__ pid, const int64_t* __restrict__ pk, const double* __restrict__ val,
@@ -533,7 +583,11 @@ __device__ __forceinline__ void onesweep_body(
   for (int i = t; i < 4 * (kHist + 1); i += kThreads) (&s_cnt[0][0])[i] = 0;
   if (TAG) s_lo[t] = tag_lo[t];
   __syncthreads();
-  const int64_t tile = tile_base ? (int64_t)blockIdx.x : (int64_t)s_tile;
+  // Reduce-then-scan: any tile order is valid, so blocks that share an XCD
+  // (blockIdx % 8, round-robin dispatch) take one contiguous run of tiles:
+  // neighbouring tiles' runs of a digit are then written through one L2.
+  const int64_t tile = tile_base ? (ks.xcd_remap ? (int64_t)xcd_tile(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x)
+                                 : (int64_t)s_tile;
   // prefetch this tile's digit bases (their latency hides behind the loads)
   const unsigned int tb = (tile_base && t < 256) ? tile_base[tile * 256 + t] : 0u;
   const int64_t n_eff = SOA ? n_in : (int64_t)counters_n[n_slot];
@@ -545,43 +599,81 @@ __device__ __forceinline__ void onesweep_body(
   Rec r[kItems];
   uint32_t dr[kItems];  // digit (9 bits) | rank in wave << 9; later the sorted position
   const int64_t base = tile_start + (int64_t)wave * (kItems * 64) + lane;
+  // Loads first, all of them in flight at once: indices are clamped (a
+  // padding item re-reads the tile's last row and is marked 257 below), so
+  // no load sits under a divergent branch.  With the loads inside the
+  // per-item `idx < n` branch the compiler waited for each item's load before
+  // issuing the next one (16 serial HBM round trips per tile).
+  const bool full = tile_start + kTile <= n_eff;
+  const int64_t last = n_eff - 1;
+  uint32_t ninv = 0;
+  if constexpr (SOA) {
 #pragma unroll
-  for (int k = 0; k < kItems; ++k) {
-    const int64_t idx = base + k * 64;
-    uint32_t d = 257;  // ignore
-    if (idx < n_eff) {
-      if (SOA) {
-        const int64_t a = pid[idx], b = pk[idx];
-        r[k].pid = (uint32_t)a;
-        r[k].pk = (uint32_t)b;
-        r[k].val = val ? val[idx] : 0.0;
-        if constexpr (TAG) {
-          // placed unless the privacy id is out of range (k_histogram_tiles<true>); a non-public row
-          // (pk < 0) is tagged dropped, an out-of-range pk is an error
-          if (a < 0 || a >= (int64_t)ks.num_pids) {
-            d = 256;
-          } else {
-            d = digit_of(ks, pass, r[k]);
-            if (b < 0 || b >= (int64_t)ks.num_parts) {
-              if (b >= 0) atomicAdd(&counters[kCtrInvalid], 1ull);
-              r[k].pid = kTagDropped | (d << 22);
-            } else {
-              r[k].pid = (d << 22) | ((r[k].pid - s_lo[d]) << 5) | filt_level(filt_prio(ks.seed, r[k].pid, r[k].pk));
-            }
-          }
+   for (int g = 0; g < kItems; g += kSoaGroup) {
+    int64_t a[kItems], b[kItems];
+#pragma unroll
+    for (int k = g; k < g + kSoaGroup; ++k) {
+      const int64_t idx = base + k * 64;
+      const int64_t ic = full ? idx : (idx < last ? idx : last);
+      a[k] = pid[ic];
+      b[k] = pk[ic];
+    }
+    if (val) {
+#pragma unroll
+      for (int k = g; k < g + kSoaGroup; ++k) {
+        const int64_t idx = base + k * 64;
+        r[k].val = val[full ? idx : (idx < last ? idx : last)];
+      }
+    } else {
+#pragma unroll
+      for (int k = g; k < g + kSoaGroup; ++k) r[k].val = 0.0;
+    }
+#pragma unroll
+    for (int k = g; k < g + kSoaGroup; ++k) {
+      uint32_t d;
+      const bool valid = full || base + k * 64 <= last;
+      r[k].pid = (uint32_t)a[k];
+      r[k].pk = (uint32_t)b[k];
+      if constexpr (TAG) {
+        // placed unless the privacy id is out of range (k_histogram_tiles<true>); a non-public row
+        // (pk < 0) is tagged dropped, an out-of-range pk is an error
+        if (a[k] < 0 || a[k] >= (int64_t)ks.num_pids) {
+          d = 256;
         } else {
-          if (b < 0 || b >= (int64_t)ks.num_parts || a < 0 || a >= (int64_t)ks.num_pids)
-            d = 256;  // dropped
-          else
-            d = digit_of(ks, pass, r[k]);
+          d = digit_of(ks, pass, r[k]);
+          if (b[k] < 0 || b[k] >= (int64_t)ks.num_parts) {
+            ninv += valid && b[k] >= 0;
+            r[k].pid = kTagDropped | (d << 22);
+          } else {
+            r[k].pid = (d << 22) | ((r[k].pid - s_lo[d]) << 5) | filt_level(filt_prio(ks.seed, r[k].pid, r[k].pk));
+          }
         }
       } else {
-        r[k] = idx < split ? ld_rec(rin + idx) : ld_rec(rin2 + (idx - split));
-        d = (ks.mode == 6 && r[k].pid == kK4EmptyKey) ? 256u : digit_of(ks, pass, r[k]);  // K4: empty slot
+        if (b[k] < 0 || b[k] >= (int64_t)ks.num_parts || a[k] < 0 || a[k] >= (int64_t)ks.num_pids)
+          d = 256;  // dropped
+        else
+          d = digit_of(ks, pass, r[k]);
       }
+      dr[k] = valid ? d : 257u;  // 257: padding, ignored
     }
-    dr[k] = d;
+   }
+  } else {
+#pragma unroll
+   for (int g = 0; g < kItems; g += kRecGroup) {
+#pragma unroll
+    for (int k = g; k < g + kRecGroup; ++k) {
+      const int64_t idx = base + k * 64;
+      const int64_t ic = full ? idx : (idx < last ? idx : last);
+      r[k] = ld_rec(ic < split ? rin + ic : rin2 + (ic - split));
+    }
+#pragma unroll
+    for (int k = g; k < g + kRecGroup; ++k) {
+      const uint32_t d = (ks.mode == 6 && r[k].pid == kK4EmptyKey) ? 256u : digit_of(ks, pass, r[k]);  // K4: empty slot
+      dr[k] = (full || base + k * 64 <= last) ? d : 257u;
+    }
+   }
   }
+  if (TAG && ninv) atomicAdd(&counters[kCtrInvalid], (unsigned long long)ninv);
 
   long long ca = 0;
   if (ks.prof) {
@@ -1638,6 +1730,7 @@ int sort_recs(pdp_ctx* ctx, Rec* a, Rec* b, int64_t m, const KeySpec& ks, unsign
 
 KeySpec composite_spec(int mode, int hi_bits, int lo_bits, int pkb, uint64_t U, uint32_t P) {
   KeySpec ks{};
+  ks.xcd_remap = env_int("PDP_XCD_REMAP", 1);
   ks.mode = mode;
   ks.low = 0;
   ks.pkb = pkb;
@@ -2064,6 +2157,7 @@ int k4_run(pdp_ctx* ctx, hipStream_t stream, const K4Plan& k, const K4Red& kr, b
   hipLaunchKernelGGL(k4_set_counter, dim3(1), dim3(64), 0, stream, counters, (int)kCtrK4In,
                      (unsigned long long)total);
   KeySpec ks{};
+  ks.xcd_remap = env_int("PDP_XCD_REMAP", 1);
   ks.mode = 6;
   ks.cap = std::min<int64_t>(total, buf_cap);  // the pairs (< total) land in buf1 / buf2
   ks.low = kr.sh;
@@ -2239,6 +2333,7 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
 
   sp.packed = !k4.on && sp.want_count && n < (1ll << 32);
   KeySpec ks{};
+  ks.xcd_remap = env_int("PDP_XCD_REMAP", 1);
   ks.mode = 0;
   ks.low = plan.low;
   ks.pkb = plan.pkb;
@@ -2675,6 +2770,7 @@ int analysis_impl(pdp_ctx* ctx, const int64_t* pid, const int64_t* pk, const dou
       // pre-aggregated pairs -> sorted by pk
       hipLaunchKernelGGL(k_ana_pack_pre, dim3(g), dim3(kThreads), 0, stream, pk, val, n, P, ra, counters);
       KeySpec ks{};
+      ks.xcd_remap = env_int("PDP_XCD_REMAP", 1);
       ks.mode = 0;
       ks.num_pids = 0xFFFFFFFFu;
       ks.num_parts = (uint32_t)P;
