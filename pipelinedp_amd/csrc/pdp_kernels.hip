@@ -2814,8 +2814,18 @@ int analysis_impl(pdp_ctx* ctx, const int64_t* pid, const int64_t* pk, const dou
   const unsigned cgroups = (unsigned)((nconf + 63) / 64);
   if (M > 0) {
     const int64_t waves = (M + kAnaChunk - 1) / kAnaChunk;
-    hipLaunchKernelGGL(k_ana_metrics, dim3((unsigned)((waves + 3) / 4), cgroups), dim3(256), 0, stream, ppk, pref,
-                       pcnt, psum, npart, M, cfg_d, nconf, mflags, P, out->metrics, mom);
+    decltype(&k_ana_metrics<true, true, true>) km = nullptr;
+    switch (mflags & (PDP_METRIC_SUM | PDP_METRIC_COUNT | PDP_METRIC_PRIVACY_ID_COUNT)) {
+#define PDP_KM(S, C, I)                                                                                    \
+  case (S ? PDP_METRIC_SUM : 0) | (C ? PDP_METRIC_COUNT : 0) | (I ? PDP_METRIC_PRIVACY_ID_COUNT : 0): \
+    km = k_ana_metrics<S, C, I>;                                                                          \
+    break;
+      PDP_KM(false, false, false) PDP_KM(true, false, false) PDP_KM(false, true, false) PDP_KM(true, true, false)
+      PDP_KM(false, false, true) PDP_KM(true, false, true) PDP_KM(false, true, true) PDP_KM(true, true, true)
+#undef PDP_KM
+    }
+    hipLaunchKernelGGL(km, dim3((unsigned)((waves + 3) / 4), cgroups), dim3(256), 0, stream, ppk, pref, pcnt, psum,
+                       npart, M, cfg_d, nconf, mflags, P, out->metrics, mom);
   }
   if (priv) {
     ProfScope ps_sel(ctx, PDP_STAGE_ANALYSIS_SELECT, stream);
