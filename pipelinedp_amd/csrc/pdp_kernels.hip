@@ -2632,6 +2632,7 @@ int keep_table(int selection, double eps, double delta, int64_t k, std::vector<d
 
 struct AnaLayout {
   size_t recs_a, recs_b, flags, ppk, pref, pcnt, psum, npart, pbeg, mom, cfg, keep, hist, off, counters, status, total;
+  AnaGroups groups{};  // distinct L0 values (G = 0: more than kAnaMaxGroups)
   int64_t tiles;
   std::vector<AnaCfg> cfgs;  // keep pointers are offsets until bound to the workspace
   std::vector<double> keep_all;
@@ -2675,6 +2676,20 @@ int ana_layout(int64_t n, int64_t U, int64_t P, const pdp_analysis_config* cfgs,
     g.keep = (const double*)(uintptr_t)L.keep_all.size();  // offset, bound later
     g.keep_len = (int64_t)t.size();
     L.keep_all.insert(L.keep_all.end(), t.begin(), t.end());
+    g.grp = -1;
+    for (int j = 0; j < L.groups.G; ++j)
+      if (L.groups.l0[j] == g.l0) g.grp = j;
+    if (g.grp < 0 && L.groups.G >= 0) {
+      if (L.groups.G < kAnaMaxGroups) {
+        g.grp = L.groups.G;
+        L.groups.rep[L.groups.G] = c;
+        L.groups.kmax[L.groups.G] = 0;
+        L.groups.l0[L.groups.G++] = g.l0;
+      } else {
+        L.groups.G = -1;  // too many distinct L0 values: k_ana_select<true / false>
+      }
+    }
+    if (g.grp >= 0 && L.groups.G > 0) L.groups.kmax[g.grp] = std::max(L.groups.kmax[g.grp], g.keep_len);
   }
   L.keep = take(L.keep_all.size() * 8);
   L.hist = take(kMaxPasses * kHist * 8);
@@ -2761,11 +2776,19 @@ int analysis_impl(pdp_ctx* ctx, const int64_t* pid, const int64_t* pk, const dou
       if (int rc = sort_recs(ctx, ra, rb, n, ks, hist, off, counters, status, status_bytes, workspace, stream, &sorted,
                              PDP_STAGE_ANALYSIS_SORT))
         return rc;
-      hipLaunchKernelGGL(k_ana_group_flags, dim3(g), dim3(kThreads), 0, stream, sorted, n, flags);
-      if (int rc = scan_inplace(flags, n, stream)) return rc;
-      hipLaunchKernelGGL(k_ana_pairs, dim3(g), dim3(kThreads), 0, stream, sorted, n, flags, num_sampled, ppk, pref,
-                         pcnt, psum, npart);
-      hipLaunchKernelGGL(k_ana_count_pairs, dim3(1), dim3(1), 0, stream, sorted, n, flags, num_sampled, counters);
+      if (env_int("PDP_ANA_FLAGS", 0)) {  // round-3 form: per-row flags, scan, one thread per group start
+        hipLaunchKernelGGL(k_ana_group_flags, dim3(g), dim3(kThreads), 0, stream, sorted, n, flags);
+        if (int rc = scan_inplace(flags, n, stream)) return rc;
+        hipLaunchKernelGGL(k_ana_pairs, dim3(g), dim3(kThreads), 0, stream, sorted, n, flags, num_sampled, ppk, pref,
+                           pcnt, psum, npart);
+        hipLaunchKernelGGL(k_ana_count_pairs, dim3(1), dim3(1), 0, stream, sorted, n, flags, num_sampled, counters);
+      } else {
+        const int64_t tiles = (n + kAnaTile - 1) / kAnaTile;
+        hipLaunchKernelGGL(k_ana_tile_groups, dim3((unsigned)tiles), dim3(256), 0, stream, sorted, n, flags);
+        if (int rc = scan_inplace(flags, tiles, stream)) return rc;
+        hipLaunchKernelGGL(k_ana_tile_pairs, dim3((unsigned)tiles), dim3(256), 0, stream, sorted, n, flags, num_sampled,
+                           ppk, pref, pcnt, psum, npart, counters);
+      }
     } else {
       // pre-aggregated pairs -> sorted by pk
       hipLaunchKernelGGL(k_ana_pack_pre, dim3(g), dim3(kThreads), 0, stream, pk, val, n, P, ra, counters);
@@ -2830,10 +2853,16 @@ int analysis_impl(pdp_ctx* ctx, const int64_t* pid, const int64_t* pk, const dou
   if (priv) {
     ProfScope ps_sel(ctx, PDP_STAGE_ANALYSIS_SELECT, stream);
     const int64_t blocks = std::min<int64_t>((P + kAnaSelWaves - 1) / kAnaSelWaves, 16384);
-    hipLaunchKernelGGL(k_ana_select<true>, dim3((unsigned)blocks, cgroups), dim3(64 * kAnaSelWaves), 0, stream, pref,
-                       npart, pbeg, P, cfg_d, nconf, (const double*)mom, out->prob_keep);
-    hipLaunchKernelGGL(k_ana_select<false>, dim3((unsigned)blocks, cgroups), dim3(64 * kAnaSelWaves), 0, stream, pref,
-                       npart, pbeg, P, cfg_d, nconf, (const double*)mom, out->prob_keep);
+    if (L.groups.G > 0 && !env_int("PDP_ANA_SEL_LDS", 0)) {
+      const size_t lds = (size_t)std::max(L.groups.G * 128, kAnaCdfMax) * 8;
+      hipLaunchKernelGGL(k_ana_select_grouped, dim3((unsigned)std::min<int64_t>(P, 65536), cgroups), dim3(64), lds,
+                         stream, pref, npart, pbeg, P, cfg_d, nconf, L.groups, (const double*)mom, out->prob_keep);
+    } else {  // round-3 form: one launch per regime, lanes = configurations
+      hipLaunchKernelGGL(k_ana_select<true>, dim3((unsigned)blocks, cgroups), dim3(64 * kAnaSelWaves), 0, stream, pref,
+                         npart, pbeg, P, cfg_d, nconf, (const double*)mom, out->prob_keep);
+      hipLaunchKernelGGL(k_ana_select<false>, dim3((unsigned)blocks, cgroups), dim3(64 * kAnaSelWaves), 0, stream,
+                         pref, npart, pbeg, P, cfg_d, nconf, (const double*)mom, out->prob_keep);
+    }
   }
   HIP_TRY(hipGetLastError());
   return 0;

@@ -40,13 +40,13 @@ def test_gpu_reference_known_answers():
         assert v[1].std_noise == pytest.approx(11.95312, abs=1e-5)
 
 
-def _cfgs(rng, C, private):
+def _cfgs(rng, C, private, l0_choices=None):
     from pipelinedp_amd import native
     sel = [native.SELECTION_TRUNCATED_GEOMETRIC, native.SELECTION_LAPLACE, native.SELECTION_GAUSSIAN]
     out = []
     for c in range(C):
         a = native.AnalysisConfig()
-        a.max_partitions_contributed = int(rng.integers(1, 40))
+        a.max_partitions_contributed = int(rng.integers(1, 40) if l0_choices is None else rng.choice(l0_choices))
         a.max_contributions_per_partition = int(rng.integers(1, 6))
         a.min_sum_per_partition = float(rng.uniform(-5, 1))
         a.max_sum_per_partition = float(a.min_sum_per_partition + rng.uniform(0.1, 8))
@@ -57,17 +57,20 @@ def _cfgs(rng, C, private):
     return out
 
 
+# grouped: at most 5 distinct L0 values, so the selection runs in
+# k_ana_select_grouped (one pmf / CDF table per L0); otherwise (> 16 distinct
+# L0 values at C = 64, 70) in k_ana_select<true / false>.
 @pytest.mark.parametrize("private", [True, False])
-@pytest.mark.parametrize("C", [1, 64, 70])
-def test_analysis_matches_oracle_many_configs(ex, private, C):
+@pytest.mark.parametrize("C,grouped", [(1, False), (64, False), (70, False), (64, True), (70, True)])
+def test_analysis_matches_oracle_many_configs(ex, private, C, grouped):
     import torch
     from pipelinedp_amd import native
-    rng = np.random.default_rng(C + 100 * private)
+    rng = np.random.default_rng(C + 100 * private + 7 * grouped)
     n, U, P = 40000, 1500, 400
     pid, pk, val = o.synth_rows(n, U, P, seed=C, zipf_s=1.1)
     if not private:
         pk = np.where(pk % 7 == 3, -1, pk)  # non-public rows
-    cfgs = _cfgs(rng, C, private)
+    cfgs = _cfgs(rng, C, private, [1, 3, 8, 20, 39] if grouped else None)
     mask = native.METRIC_SUM | native.METRIC_COUNT | native.METRIC_PRIVACY_ID_COUNT
     t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
     metrics, prob, pids = ex.analyze(t(pid), t(pk), t(val), U, P, mask, cfgs)
