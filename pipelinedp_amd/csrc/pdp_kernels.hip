@@ -46,6 +46,9 @@ constexpr int kThreads = 256;
 #endif
 constexpr int kItems = PDP_OS_ITEMS;         // rows per thread in a radix tile
 constexpr int kTile = kThreads * kItems;     // 4096 rows per radix tile
+// Other tile sizes are not supported: a 12-rows-per-thread build (3072-row
+// tiles) faulted on the GPU in the pre-filter path (round-3 experiment).
+static_assert(kTile == 4096, "the radix / filter kernels assume 4096-row tiles");
 constexpr int kMaxPasses = 12;
 constexpr int kHist = 257;                   // 256 digits + drop bucket
 constexpr int kStatusStride = 256;
