@@ -36,6 +36,10 @@ PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 WORKLOADS = {
     "c3": dict(rows=1e9, partitions=1e6, pids=1e7, zipf=1.1, l0=4, linf=2, public=False, metrics="mean",
                cpu_sample=6e6, strong=True),  # CPU baseline rows per host core
+    # c3v: BASELINE configs[2] as written -- the c3 shape with MEAN + VARIANCE (+ COUNT + SUM): K2 also writes
+    # the y slot array and K4 runs a second (y) reduction
+    "c3v": dict(rows=1e9, partitions=1e6, pids=1e7, zipf=1.1, l0=4, linf=2, public=False, metrics="variance",
+                cpu_sample=6e6, strong=True),
     "c2": dict(rows=1e8, partitions=1e5, pids=1e6, zipf=0.0, l0=8, linf=4, public=True, metrics="count_sum",
                cpu_sample=6e6),
     "c4": dict(rows=5e8, partitions=5e7, pids=1.25e7, zipf=1.1, l0=32, linf=4, public=False, metrics="mean",
@@ -105,7 +109,7 @@ def parse():
     return args
 
 
-def stage_bytes(stage, n_in, n_kept, P, nfields, survivors=0, survivor_passes=0, k4=None):
+def stage_bytes(stage, n_in, n_kept, P, nfields, survivors=0, survivor_passes=0, k4=None, y_slots=False):
     """Algorithmic bytes of one launch of each kernel (Roofline).
     With the L0 pre-filter (survivors > 0): K0 reads the privacy ids only, the
     first pass is the bucket pass (+ a 4-B tag per row), k_filter reads the
@@ -114,7 +118,9 @@ def stage_bytes(stage, n_in, n_kept, P, nfields, survivors=0, survivor_passes=0,
     (k4 = (slots, pairs, passes)): K2 also writes one 16-B slot per sorted row,
     the first pair pass reads the slots and writes the pairs, later passes
     read + write the pairs, the reduction reads the pairs and writes
-    row_count / count / x (8 B each) per partition."""
+    row_count / count / x (8 B each) per partition.  VARIANCE (y_slots): K2
+    writes a second slot array and K4 runs once more on it (same bytes per
+    pair-pass / reduce launch)."""
     sorted_rows = survivors if survivors else n_kept
     slots, pairs, kpasses = k4 or (0, 0, 0)
     return {
@@ -124,7 +130,7 @@ def stage_bytes(stage, n_in, n_kept, P, nfields, survivors=0, survivor_passes=0,
         "filter": 12 * n_kept + 32 * survivors,  # tags three times, survivors' records read + written
         # histogram read + per pass (read + write) + per later pass an upsweep read
         "survivor_sort": survivors * (16 + 32 * survivor_passes + 16 * max(survivor_passes - 1, 0)),
-        "buckets": 16 * sorted_rows + 16 * slots,  # read 16-B records once (+ K4: write the pair slots)
+        "buckets": 16 * sorted_rows + (32 if y_slots else 16) * slots,  # read 16-B records once (+ K4: write the pair slots)
         "pair_pass": 16 * slots + 16 * pairs + 32 * pairs * max(kpasses - 1, 0),
         "reduce": 16 * pairs + 24 * P,
         "release": P * (3 * 8 + 1 + 8 * nfields),
@@ -203,7 +209,7 @@ def _cpu_bound(task):
     acc = o.bound_and_accumulate(pid[mine], pk[mine], val[mine], P, o.BoundParams(l0, linf, 0.0, 10.0), "hash",
                                  seed=seed)
     idx = np.flatnonzero(acc.row_count)
-    return idx, acc.row_count[idx], acc.count[idx], acc.sum[idx], acc.nsum[idx]
+    return idx, acc.row_count[idx], acc.count[idx], acc.sum[idx], acc.nsum[idx], acc.nsumsq[idx]
 
 
 def _cpu_analysis(task):
@@ -270,16 +276,20 @@ def cpu_baseline(args, P):
         pool.map(_cpu_gen, [(int(bounds[i]), int(bounds[i + 1]), U, P, args.seed, args.zipf) for i in range(W)])
         t0 = time.perf_counter()
         parts = pool.map(_cpu_bound, [(w, W, P, args.l0, args.linf, 1) for w in range(W)])
-        rc, cnt, sm, ns = (np.zeros(P, np.int64), np.zeros(P, np.int64), np.zeros(P), np.zeros(P))
-        for idx, a, b, c, d in parts:
+        rc, cnt, sm, ns, nq = (np.zeros(P, np.int64), np.zeros(P, np.int64), np.zeros(P), np.zeros(P), np.zeros(P))
+        for idx, a, b, c, d, e in parts:
             rc[idx] += a
             cnt[idx] += b
             sm[idx] += c
             ns[idx] += d
-        acc = o.Accumulators(rc, cnt, sm, ns, np.zeros(P))
+            nq[idx] += e
+        acc = o.Accumulators(rc, cnt, sm, ns, nq)
         bp = o.BoundParams(args.l0, args.linf, 0.0, 10.0)
         if WORKLOADS[args.workload]["public"]:
             spec = o.ReleaseSpec(("count", "sum"), "laplace", {"count": (0.5, 0.0), "sum": (0.5, 0.0)}, None)
+        elif metrics == "variance":
+            spec = o.ReleaseSpec(("variance", "mean", "count", "sum"), "laplace", {"variance": (0.5, 0.0)},
+                                 "truncated_geometric", (0.5, 1e-6))
         else:
             spec = o.ReleaseSpec(("mean", "count", "sum"), "laplace", {"mean": (0.5, 0.0)}, "truncated_geometric",
                                  (0.5, 1e-6))
@@ -349,7 +359,10 @@ def main():
     public = WORKLOADS[args.workload]["public"]
     count_sum = WORKLOADS[args.workload]["metrics"] == "count_sum"
     sweep = WORKLOADS[args.workload]["metrics"] == "analysis"
+    variance = WORKLOADS[args.workload]["metrics"] == "variance"
     mask = native.METRIC_COUNT | native.METRIC_SUM | (0 if count_sum else native.METRIC_MEAN)
+    if variance:
+        mask |= native.METRIC_VARIANCE
     if sweep:
         # UtilityAnalysisOptions(eps=1, delta=1e-6), metrics COUNT+SUM+PRIVACY_ID_COUNT, private selection:
         # NaiveBudgetAccountant gives the GENERIC mechanism eps 1/4 and all of delta
@@ -363,6 +376,8 @@ def main():
     delta = [0.0] * 6
     if count_sum:  # public partitions: the whole budget goes to COUNT and SUM (weights 1:1)
         eps[native.MECH_COUNT] = eps[native.MECH_SUM] = 0.5
+    elif variance:
+        eps[native.MECH_VARIANCE] = 0.5
     else:
         eps[native.MECH_MEAN] = 0.5
     if not public:
@@ -395,9 +410,11 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    marks = []
     for _ in range(args.steps):
         res = step()
-    torch.cuda.synchronize()
+        torch.cuda.synchronize()  # per-step stamps for the median (the path syncs inside each step anyway)
+        marks.append(time.perf_counter())
     if world is not None:
         dist.barrier()
     elapsed = time.perf_counter() - t0
@@ -422,7 +439,7 @@ def main():
                                   sel["ms_per_launch"] * sel["launches_per_step"]) / m["launches_per_step"]
         dom = max(stages, key=lambda s: stages[s]["ms_per_launch"] * stages[s]["launches_per_step"])
         nb = (P + world_size - 1) // world_size if world else P
-        b = stage_bytes(dom, n, rows_after_public_filter, nb, len(fields), surv, surv_passes, k4)
+        b = stage_bytes(dom, n, rows_after_public_filter, nb, len(fields), surv, surv_passes, k4, variance)
         ach = b / (stages[dom]["ms_per_launch"] * 1e-3) / 1e9
         traffic, prof_round = pmc_traffic(dom, n, args.workload) if not sweep else (None, None)
         roofline = {"bound": "hbm", "kernel": dom, "achieved": round(ach, 1), "peak": PEAK_HBM_GBS,
@@ -458,7 +475,7 @@ def main():
                         "ms_per_launch_source": "hipEvents on the launch stream (analysis_metrics minus the nested "
                                                 "analysis_select), averaged over the timed steps"}
         for s in stages:
-            bs = stage_bytes(s, n, rows_after_public_filter, nb, len(fields), surv, surv_passes, k4)
+            bs = stage_bytes(s, n, rows_after_public_filter, nb, len(fields), surv, surv_passes, k4, variance)
             if bs:
                 stages[s]["achieved_GBs"] = round(bs / (stages[s]["ms_per_launch"] * 1e-3) / 1e9, 1)
 
@@ -471,6 +488,8 @@ def main():
         del acc
 
     rows_per_s = n * world_size * args.steps / elapsed
+    step_s = sorted(b - a for a, b in zip([t0] + marks[:-1], marks))
+    med = step_s[len(step_s) // 2] if len(step_s) % 2 else 0.5 * (step_s[len(step_s) // 2 - 1] + step_s[len(step_s) // 2])
     copy_gbs = copy_peak_gbs(torch, native.lib()) if rank == 0 and not args.no_profile else None
     if roofline is not None:
         roofline["copy_peak_measured"] = copy_gbs
@@ -483,6 +502,8 @@ def main():
             "metric": "input rows/sec (node) for DP COUNT+SUM+MEAN, 1B rows/1M partitions; % HBM peak",
             "value": rows_per_s, "unit": "rows/s", "n_gpus": world_size, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+            "ms_per_step_median": med * 1e3, "value_median_step": n * world_size / med,
+            "median_note": "median of the per-step times on rank 0 (BASELINE.md: median); value = K steps / total",
             "scaling": "strong" if args.strong else "weak", "vs_baseline": None, "dtype": "f64",
             "data": "synthetic (on-device Philox generator, oracle/pdp_oracle.py:synth_rows)",
             "config": {"workload": (f"c5: UtilityAnalysisEngine.analyze, {len(SWEEP)} configurations "
@@ -490,7 +511,7 @@ def main():
                                     f"per-partition error metrics + truncated-geometric keep probability, "
                                     f"{n:.2e} rows/GPU, {U:.1e} privacy ids, {P:.1e} Zipf({args.zipf}) partitions; "
                                     f"value = input rows/s for the whole analysis") if sweep else
-                                   f"{args.workload}: DP {'COUNT+SUM' if count_sum else 'COUNT+SUM+MEAN'}, "
+                                   f"{args.workload}: DP {'COUNT+SUM' if count_sum else 'COUNT+SUM+MEAN+VARIANCE' if variance else 'COUNT+SUM+MEAN'}, "
                                    f"{n * world_size:.2e} rows on {world_size} GPU(s) ({n:.2e} rows/GPU), "
                                    f"{U:.1e} privacy ids/GPU, {P:.1e} "
                                    f"{'public uniform' if public else f'Zipf({args.zipf})'} partitions, "

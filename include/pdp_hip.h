@@ -172,6 +172,38 @@ int pdp_bound_accumulate(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_
                          const pdp_accumulators* acc, void* workspace, size_t workspace_bytes,
                          void* stream);
 
+/* Multi-GPU form of pdp_bound_accumulate: the per-partition sums are exported
+ * in K4's 64-bit fixed point instead of as doubles, so that the partials of
+ * several ranks add up exactly (an int64 SUM reduce-scatter) before ONE
+ * conversion on the owning rank -- the combine_accumulators_per_key merge
+ * (pipeline_dp/pipeline_backend.py:528-538) across GPUs, with a result that
+ * equals one GPU's bit for bit.  Per partition p:
+ *   x = (x_hi[p] + (x_lo[p] >> 32)) * 2^(32-F) + (x_lo[p] mod 2^32) * 2^-F
+ * (F from the contribution bounds, pdp_finalize_partials applies it); x_lo is
+ * in [0, 2^32) per rank.  nan[p] counts NaN terms: + 1 per x NaN, + 2^32 per
+ * y NaN.  Arrays are [num_partitions] int64; row_count / count / x_* / y_* /
+ * nan as the metrics need them (x: SUM / MEAN / VARIANCE, y: VARIANCE, nan:
+ * with x).  Needs the K4 reduction (num_rows < 2^32). */
+typedef struct pdp_partials {
+  int64_t* row_count;
+  int64_t* count;
+  int64_t* x_hi;
+  int64_t* x_lo;
+  int64_t* y_hi;
+  int64_t* y_lo;
+  int64_t* nan;
+} pdp_partials;
+
+int pdp_bound_accumulate_partials(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp,
+                                  const pdp_partials* parts, void* workspace, size_t workspace_bytes,
+                                  void* stream);
+
+/* Summed partials of num_partitions partitions -> accumulators for
+ * pdp_release (bp: the bounds pdp_bound_accumulate_partials ran with).
+ * acc->row_count / count may alias parts->row_count / count (then no copy). */
+int pdp_finalize_partials(pdp_ctx* ctx, const pdp_partials* parts, int64_t num_partitions,
+                          const pdp_bound_params* bp, const pdp_accumulators* acc, void* stream);
+
 /* Bounding sweep (utility analysis over many bounding configurations, the
  * per-configuration DPEngine runs of analysis/utility_analysis_engine.py:
  * 88-173 with MultiParameterConfiguration, analysis/data_structures.py):

@@ -429,6 +429,9 @@ class Accumulators:
     nsumsq: np.ndarray
     kept_rows: int = 0
     kept_pairs: int = 0
+    # the kept (pid, pk) accumulators before the per-partition merge:
+    # (pk, count, sum, nsum, nsumsq) arrays, one entry per kept pair
+    pairs: Optional[tuple] = None
 
 
 def _group_starts(keys_sorted_list):
@@ -544,9 +547,16 @@ def bound_and_accumulate(pid, pk, value, num_partitions, params: BoundParams,
             elif have_pb:
                 s = np.bincount(pkk, weights=np.clip(v, params.min_sum_per_partition,
                                                      params.max_sum_per_partition), minlength=P)
+        m = len(pkk)
+        ps = pns = pnsq = np.zeros(m)
+        if value is not None and have_vb:
+            ps, pns, pnsq = cv, nv, nv * nv
+        elif value is not None and have_pb:
+            ps = np.clip(v, params.min_sum_per_partition, params.max_sum_per_partition)
         return Accumulators(row_count, count, np.asarray(s, np.float64),
                             np.asarray(ns, np.float64), np.asarray(nsq, np.float64),
-                            int(keep_row.sum()), int(keep_row.sum()))
+                            int(keep_row.sum()), int(keep_row.sum()),
+                            pairs=(pkk, np.ones(m, np.int64), ps, pns, pnsq))
 
     pid = np.asarray(pid, dtype=np.int64)[keep_row]
     pk = pk[keep_row]
@@ -629,8 +639,106 @@ def bound_and_accumulate(pid, pk, value, num_partitions, params: BoundParams,
         nsum=np.bincount(kp, weights=g_nsum[gkeep], minlength=P),
         nsumsq=np.bincount(kp, weights=g_nsq[gkeep], minlength=P),
         kept_rows=int(g_count[gkeep].sum()),
-        kept_pairs=int(gkeep.sum()))
+        kept_pairs=int(gkeep.sum()),
+        pairs=(kp, g_count[gkeep], g_sum[gkeep], g_nsum[gkeep], g_nsq[gkeep]))
     return acc
+
+
+# ----------------------------------------------------------------------------
+# K4 fixed point (pipelinedp_amd/csrc/pdp_reduce.inc): the per-partition merge
+# of the pair accumulators (combine_accumulators_per_key,
+# pipeline_backend.py:528-538) in 64-bit fixed point, and its multi-GPU
+# export (pdp_bound_accumulate_partials / pdp_finalize_partials)
+# ----------------------------------------------------------------------------
+
+METRIC_BITS = {"count": 1, "sum": 2, "mean": 4, "variance": 8, "privacy_id_count": 16}
+
+
+def k4_exponent(M):
+    """F = 62 - ceil(log2 M) (k4_exponent: frexp's e, M < 2^e), clamped."""
+    if not (M > 0.0) or not math.isfinite(M):
+        return 0
+    _, e = math.frexp(M)
+    return max(-1000, min(1000, 62 - e))
+
+
+def k4_exponents(params: BoundParams, metrics_mask):
+    """(F_x, F_y, x kind) as k4_plan / make_seg pick them: the largest |x| of
+    one pair is L_inf (b - a) / 2 for normalised sums (MEAN / VARIANCE),
+    L_inf max(|a|, |b|) for clipped SUM, max(|min_sum|, |max_sum|) for SUM
+    with per-partition sum bounds; y: L_inf ((b - a) / 2)^2."""
+    linf = 1.0 if params.contribution_bounds_already_enforced else float(params.max_contributions_per_partition)
+    a = params.min_value if params.min_value is not None else 0.0
+    b = params.max_value if params.max_value is not None else 0.0
+    half = abs(b - a) / 2.0
+    m = metrics_mask
+    if m & (METRIC_BITS["mean"] | METRIC_BITS["variance"]):
+        kind, mx = "nsum", linf * half
+    elif m & METRIC_BITS["sum"]:
+        if params.min_value is not None:
+            kind, mx = "sum", linf * max(abs(a), abs(b))
+        else:
+            kind, mx = "sum", max(abs(params.min_sum_per_partition or 0.0), abs(params.max_sum_per_partition or 0.0))
+    else:
+        kind, mx = None, 0.0
+    return k4_exponent(mx), k4_exponent(linf * half * half), kind
+
+
+def k4_fixed_sums(pair_pk, pair_x, num_partitions, F):
+    """Exported fixed-point sums (hi, lo, nan count) [P] of the pair values:
+    q = rint(x 2^F) per pair, hi = sum(q >> 32) + (sum(q mod 2^32) >> 32),
+    lo = sum(q mod 2^32) mod 2^32 (pdp_hip.h pdp_partials)."""
+    P = int(num_partitions)
+    x = np.asarray(pair_x, np.float64)
+    pk = np.asarray(pair_pk, np.int64)
+    isnan = np.isnan(x)
+    q = np.rint(np.where(isnan, 0.0, x) * math.ldexp(1.0, F)).astype(np.int64)
+    hi = np.zeros(P, np.int64)
+    lo = np.zeros(P, np.int64)
+    np.add.at(hi, pk, q >> 32)
+    np.add.at(lo, pk, q & 0xFFFFFFFF)
+    hi += lo >> 32
+    lo &= 0xFFFFFFFF
+    return hi, lo, np.bincount(pk[isnan], minlength=P).astype(np.int64)
+
+
+def k4_to_double(hi, lo, nan, F):
+    """(summed) fixed-point partials -> fp64 (k4_value): h = hi + (lo >> 32),
+    l = lo mod 2^32, h 2^(32-F) + l 2^-F; NaN where a NaN term was added."""
+    hi = np.asarray(hi, np.int64)
+    lo = np.asarray(lo, np.int64)
+    h = hi + (lo >> 32)
+    v = h.astype(np.float64) * math.ldexp(1.0, 32 - F) + (lo & 0xFFFFFFFF).astype(np.float64) * math.ldexp(1.0, -F)
+    return np.where(np.asarray(nan) != 0, np.nan, v)
+
+
+PARTIAL_FIELDS = ("row_count", "count", "x_hi", "x_lo", "nan", "y_hi", "y_lo")
+
+
+def k4_partials(acc: Accumulators, num_partitions, params: BoundParams, metrics_mask):
+    """The rank-local partials of pdp_bound_accumulate_partials from an
+    oracle result: {field: int64 [P]} (nan: + 1 per x NaN, + 2^32 per y NaN)."""
+    fx, fy, kind = k4_exponents(params, metrics_mask)
+    pk, _, s, ns, nsq = acc.pairs
+    out = {"row_count": acc.row_count.astype(np.int64), "count": acc.count.astype(np.int64)}
+    if kind is not None:
+        out["x_hi"], out["x_lo"], nx = k4_fixed_sums(pk, ns if kind == "nsum" else s, num_partitions, fx)
+        out["nan"] = nx
+    if metrics_mask & METRIC_BITS["variance"]:
+        out["y_hi"], out["y_lo"], ny = k4_fixed_sums(pk, nsq, num_partitions, fy)
+        out["nan"] = out["nan"] + (ny << 32)
+    return out
+
+
+def k4_finalize(parts, params: BoundParams, metrics_mask):
+    """pdp_finalize_partials restated: -> (x, y) fp64 arrays (None if absent)."""
+    fx, fy, kind = k4_exponents(params, metrics_mask)
+    x = y = None
+    if kind is not None:
+        x = k4_to_double(parts["x_hi"], parts["x_lo"], parts["nan"] & 0xFFFFFFFF, fx)
+    if metrics_mask & METRIC_BITS["variance"]:
+        y = k4_to_double(parts["y_hi"], parts["y_lo"], parts["nan"] >> 32, fy)
+    return x, y
 
 
 # ----------------------------------------------------------------------------

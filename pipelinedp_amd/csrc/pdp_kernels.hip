@@ -438,7 +438,7 @@ __global__ __launch_bounds__(kThreads) void k_tile_counts(const Rec* __restrict_
 #pragma unroll
       for (int u = 0; u < kHistUnroll; ++u) {
         const int64_t i = base + (int64_t)(g + u) * kThreads;
-        r[u] = rin[i < n ? i : n - 1];
+        if (n > 0) r[u] = rin[i < n ? i : n - 1];  // n == 0 (every row dropped): no load at all
       }
 #pragma unroll
       for (int u = 0; u < kHistUnroll; ++u)
@@ -1067,14 +1067,21 @@ __global__ void k_stream_ranks(const Rec* __restrict__ sorted, int64_t m, const 
 
 // Kept groups: the L_inf-kept rows of each L0-kept group summed in input
 // order (deterministic), then one accumulator add (or, K4, one pair record in
-// slot g of the generic path's pair array; sp.k4x / k4y point there).
+// slot g of the generic path's pair array; sp.k4x / k4y point there).  A kept
+// group of more than kBigGroupRows rows (a heavy privacy id in one partition)
+// is not walked by one lane: it goes to `big` for k_stream_big_groups.
+constexpr int64_t kBigGroupRows = 2048;
 __global__ void k_stream_groups(const Rec* __restrict__ r, const long long* __restrict__ gpos,
                                 const int32_t* __restrict__ grank, const uint8_t* __restrict__ row_keep,
-                                int64_t ngroups, SegParams sp, AccPtrs acc) {
+                                int64_t ngroups, SegParams sp, AccPtrs acc, unsigned long long* __restrict__ big) {
   for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < ngroups;
        g += (int64_t)gridDim.x * blockDim.x) {
     uint32_t c = 0;
     double x = 0.0, y = 0.0;
+    if (grank[g] < sp.l0 && gpos[g + 1] - gpos[g] > kBigGroupRows) {
+      big[1 + atomicAdd(&big[0], 1ull)] = (unsigned long long)g;  // big[0]: count, then the group ids
+      continue;
+    }
     if (grank[g] < sp.l0) {
       for (long long q = gpos[g]; q < gpos[g + 1]; ++q) {
         if (!row_keep[q]) continue;
@@ -1090,6 +1097,66 @@ __global__ void k_stream_groups(const Rec* __restrict__ r, const long long* __re
       else k4_empty(sp, g);
     } else if (c > 0) {
       emit_group(sp, acc, r[gpos[g]].pk, c, x, y);
+    }
+  }
+}
+
+// The big kept groups: one block per group.  Each round the block reads 256
+// consecutive rows (coalesced keep bytes), each thread adds its kept row's
+// terms, and a fixed-shape block tree sums the round; round sums are added in
+// row order.  The order depends only on the group's rows, so the result is
+// identical run to run (it is not the sequential input-order sum of
+// k_stream_groups: fp64 sums differ from it in the last bits).
+__global__ __launch_bounds__(kThreads) void k_stream_big_groups(const Rec* __restrict__ r,
+                                                                const long long* __restrict__ gpos,
+                                                                const uint8_t* __restrict__ row_keep, SegParams sp,
+                                                                AccPtrs acc, const unsigned long long* __restrict__ big) {
+  __shared__ double s_x[kThreads / 64], s_y[kThreads / 64];
+  __shared__ unsigned int s_c[kThreads / 64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t nbig = (int64_t)big[0];
+  for (int64_t b = blockIdx.x; b < nbig; b += gridDim.x) {
+    const int64_t g = (int64_t)big[1 + b];
+    const long long q0 = gpos[g], q1 = gpos[g + 1];
+    uint32_t c = 0;
+    double x = 0.0, y = 0.0;
+    for (long long base = q0; base < q1; base += kThreads) {
+      const long long q = base + threadIdx.x;
+      double xt = 0.0, yt = 0.0;
+      unsigned int ct = 0;
+      if (q < q1 && row_keep[q]) {
+        row_terms(sp, r[q].val, xt, yt);
+        ct = 1;
+      }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        xt += __shfl_down(xt, o);
+        yt += __shfl_down(yt, o);
+        ct += __shfl_down(ct, o);
+      }
+      if (lane == 0) {
+        s_x[w] = xt;
+        s_y[w] = yt;
+        s_c[w] = ct;
+      }
+      __syncthreads();
+      if (threadIdx.x == 0) {
+#pragma unroll
+        for (int i = 0; i < kThreads / 64; ++i) {
+          x += s_x[i];
+          y += s_y[i];
+          c += s_c[i];
+        }
+      }
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+      if (sp.k4x) {
+        if (c > 0) k4_put(sp, g, r[q0].pk, c, x, y, sp.k4hist);
+        else k4_empty(sp, g);
+      } else if (c > 0) {
+        emit_group(sp, acc, r[q0].pk, c, x, y);
+      }
     }
   }
 }
@@ -1360,20 +1427,43 @@ __global__ __launch_bounds__(256) void k_fp64_probe(double* __restrict__ out, in
   if (s == 12345.678) out[blockIdx.x] = s;  // keeps the chains alive
 }
 
-// Variant: 8 loads in flight per lane, non-temporal loads and stores (streaming data that is never
-// re-read should not displace L2 / Infinity-Cache lines).
-__global__ __launch_bounds__(256) void k_stream_copy_nt(const u32x4* __restrict__ src, u32x4* __restrict__ dst,
-                                                        int64_t n16) {
+// Variants: 8 loads in flight per lane; NTL / NTS = non-temporal loads / stores (streaming data that is
+// never re-read should not displace L2 / Infinity-Cache lines).  RD: read only (the XOR of the loaded
+// words stays in a register; one store per lane if it equals a magic value), WR: write only.
+enum CopyKind { kCopyRW = 0, kCopyRead = 1, kCopyWrite = 2 };
+template <bool NTL, bool NTS, int KIND>
+__global__ __launch_bounds__(256) void k_stream_copy_8(const u32x4* __restrict__ src, u32x4* __restrict__ dst,
+                                                       int64_t n16) {
   const int64_t stride = (int64_t)gridDim.x * 256;
   int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  uint32_t acc = 0;
   for (; i + 7 * stride < n16; i += 8 * stride) {
     u32x4 v[8];
+    if (KIND != kCopyWrite) {
 #pragma unroll
-    for (int k = 0; k < 8; ++k) v[k] = __builtin_nontemporal_load(src + i + k * stride);
+      for (int k = 0; k < 8; ++k) v[k] = NTL ? __builtin_nontemporal_load(src + i + k * stride) : src[i + k * stride];
+    } else {
 #pragma unroll
-    for (int k = 0; k < 8; ++k) __builtin_nontemporal_store(v[k], dst + i + k * stride);
+      for (int k = 0; k < 8; ++k) v[k] = u32x4{(uint32_t)i, (uint32_t)k, 0u, 0u};
+    }
+    if (KIND == kCopyRead) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc ^= v[k].x ^ v[k].y ^ v[k].z ^ v[k].w;
+    } else {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        if (NTS) __builtin_nontemporal_store(v[k], dst + i + k * stride);
+        else dst[i + k * stride] = v[k];
+      }
+    }
   }
-  for (; i < n16; i += stride) dst[i] = src[i];
+  for (; i < n16; i += stride) {
+    if (KIND == kCopyRead) acc ^= src[i].x;
+    else if (KIND == kCopyWrite) dst[i] = u32x4{(uint32_t)i, 0u, 0u, 0u};
+    else dst[i] = src[i];
+  }
+  const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (KIND == kCopyRead && acc == 0x9E3779B9u && j < n16) dst[j] = u32x4{acc, 0u, 0u, 0u};
 }
 
 // ---------------------------------------------------------------------------
@@ -1855,8 +1945,13 @@ int run_generic(pdp_ctx* ctx, const Rec* sorted, Rec* spare, Rec* alt, const std
     *kf_y = sp.k4y;
     *kf_n = ngroups;
   }
+  unsigned long long* big = nullptr;  // [count, group ids]: kept groups over kBigGroupRows rows
+  HIP_TRY(scratch.alloc((void**)&big, (size_t)(total / kBigGroupRows + 2) * 8));
+  HIP_TRY(hipMemsetAsync(big, 0, 8, stream));
   hipLaunchKernelGGL(k_stream_groups, dim3(ggr), dim3(kThreads), 0, stream, r, gpos, grank, row_keep,
-                     (int64_t)ngroups, sp, acc);
+                     (int64_t)ngroups, sp, acc, big);
+  hipLaunchKernelGGL(k_stream_big_groups, dim3((unsigned)std::min<int64_t>(total / kBigGroupRows + 1, 1024)),
+                     dim3(kThreads), 0, stream, r, gpos, row_keep, sp, acc, big);
   HIP_TRY(hipGetLastError());
   (void)r_other;
   return 0;
@@ -2219,8 +2314,10 @@ int k4_run(pdp_ctx* ctx, hipStream_t stream, const K4Plan& k, const K4Red& kr, b
 // order does not depend on L0 / L_inf / clipping), then K2 (+ KF) runs per
 // configuration over the same sorted rows.
 int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bps, int nconf,
-               const pdp_accumulators* accps, void* workspace, size_t workspace_bytes, void* stream_, bool sweep) {
+               const pdp_accumulators* accps, void* workspace, size_t workspace_bytes, void* stream_, bool sweep,
+               const pdp_partials* parts = nullptr) {
   if (!ctx || !cols || !bps || !accps) return fail(PDP_ERR_INVALID_ARG, "null argument");
+  if (parts && (sweep || nconf != 1)) return fail(PDP_ERR_INVALID_ARG, "partials: one configuration, no sweep");
   if (nconf < 1) return fail(PDP_ERR_INVALID_ARG, "num_configs must be >= 1");
   DeviceGuard dg(ctx->device);
   if (!dg.ok) return fail(PDP_ERR_HIP, "hipSetDevice failed");
@@ -2246,6 +2343,14 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
     if (!a->row_count) return fail(PDP_ERR_INVALID_ARG, "row_count accumulator required");
     sps[c] = make_seg(b, plan.low, plan.pkb, cols->value != nullptr);
     if (sps[c].want_count && !a->count) return fail(PDP_ERR_INVALID_ARG, "count accumulator required");
+    if (parts) {
+      if (sps[c].xmode != kXNone && (!parts->x_hi || !parts->x_lo || !parts->nan))
+        return fail(PDP_ERR_INVALID_ARG, "x_hi / x_lo / nan partials required");
+      if (sps[c].want_y && (!parts->y_hi || !parts->y_lo))
+        return fail(PDP_ERR_INVALID_ARG, "y_hi / y_lo partials required");
+      accs[c] = AccPtrs{(unsigned long long*)a->row_count, (unsigned long long*)a->count, nullptr, nullptr};
+      continue;
+    }
     if (sps[c].xmode != kXNone && !a->x) return fail(PDP_ERR_INVALID_ARG, "x accumulator required");
     if (sps[c].want_y && !a->y) return fail(PDP_ERR_INVALID_ARG, "y accumulator required");
     accs[c] = AccPtrs{(unsigned long long*)a->row_count, (unsigned long long*)a->count, a->x, a->y};
@@ -2263,9 +2368,14 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
     if (a.x) HIP_TRY(hipMemsetAsync(a.x, 0, (size_t)P * 8, stream));
     if (a.y) HIP_TRY(hipMemsetAsync(a.y, 0, (size_t)P * 8, stream));
   }
+  if (parts) {
+    for (int64_t* t : {parts->x_hi, parts->x_lo, parts->y_hi, parts->y_lo, parts->nan})
+      if (t) HIP_TRY(hipMemsetAsync(t, 0, (size_t)P * 8, stream));
+  }
   if (n == 0) return 0;
 
   const K4Plan k4 = k4_plan(bp, sp, n, P, sweep);
+  if (parts && !k4.on) return fail(PDP_ERR_INVALID_ARG, "partials need the K4 reduction (num_rows < 2^32, PDP_K4 on)");
   const Layout L = layout_for(n, sweep, k4.on ? P : 0, sp.want_y != 0);
   if (!workspace || workspace_bytes < L.total) return fail(PDP_ERR_WORKSPACE, "workspace too small");
   char* ws = (char*)workspace;
@@ -2304,12 +2414,23 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
     hipLaunchKernelGGL(k4_offsets, dim3(1), dim3(kThreads), 0, stream, k4rep, k4.passes, off, counters);
     ctx->stats.k4_slots = nslots + nkf;
     ctx->stats.k4_passes = k4.passes;
-    if (int rc = k4_run(ctx, stream, k4, k4_red(k4, q, P, false), false, slots, nslots, kfx, nkf, buf1, buf2, acc, off,
-                        counters, status, workspace, k4lo, k4hi, k4fl, n))
+    K4Red krx = k4_red(k4, q, P, false), kry = k4_red(k4, q, P, true);
+    if (parts) {  // fixed-point export (multi-GPU partials)
+      krx.fxh = (long long*)parts->x_hi;
+      krx.fxl = (long long*)parts->x_lo;
+      krx.fxn = (unsigned long long*)parts->nan;
+      krx.nan_inc = 1ull;
+      kry.fxh = (long long*)parts->y_hi;
+      kry.fxl = (long long*)parts->y_lo;
+      kry.fxn = (unsigned long long*)parts->nan;
+      kry.nan_inc = 1ull << 32;
+    }
+    if (int rc = k4_run(ctx, stream, k4, krx, false, slots, nslots, kfx, nkf, buf1, buf2, acc, off, counters, status,
+                        workspace, k4lo, k4hi, k4fl, n))
       return rc;
     if (q.want_y) {
-      if (int rc = k4_run(ctx, stream, k4, k4_red(k4, q, P, true), true, k4y, nslots, kfy, nkf, buf1, buf2, acc, off,
-                          counters, status, workspace, k4lo, k4hi, k4fl, n))
+      if (int rc = k4_run(ctx, stream, k4, kry, true, k4y, nslots, kfy, nkf, buf1, buf2, acc, off, counters, status,
+                          workspace, k4lo, k4hi, k4fl, n))
         return rc;
     }
     return 0;
@@ -2878,6 +2999,46 @@ int pdp_bound_accumulate(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_
   return bound_impl(ctx, cols, bp, 1, accp, workspace, workspace_bytes, stream, false);
 }
 
+int pdp_bound_accumulate_partials(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp,
+                                  const pdp_partials* parts, void* workspace, size_t workspace_bytes, void* stream) {
+  if (!parts) return fail(PDP_ERR_INVALID_ARG, "null argument");
+  const pdp_accumulators a{parts->row_count, parts->count, nullptr, nullptr};
+  return bound_impl(ctx, cols, bp, 1, &a, workspace, workspace_bytes, stream, false, parts);
+}
+
+int pdp_finalize_partials(pdp_ctx* ctx, const pdp_partials* parts, int64_t P, const pdp_bound_params* bp,
+                          const pdp_accumulators* acc, void* stream_) {
+  if (!ctx || !parts || !bp || !acc) return fail(PDP_ERR_INVALID_ARG, "null argument");
+  if (P < 0) return fail(PDP_ERR_INVALID_ARG, "num_partitions < 0");
+  DeviceGuard dg(ctx->device);
+  if (!dg.ok) return fail(PDP_ERR_HIP, "hipSetDevice failed");
+  hipStream_t stream = (hipStream_t)stream_;
+  const SegParams sp = make_seg(bp, 0, 1, true);
+  if (!parts->row_count || !acc->row_count) return fail(PDP_ERR_INVALID_ARG, "row_count required");
+  if (sp.want_count && (!parts->count || !acc->count)) return fail(PDP_ERR_INVALID_ARG, "count required");
+  if (sp.xmode != kXNone && (!parts->x_hi || !parts->x_lo || !acc->x)) return fail(PDP_ERR_INVALID_ARG, "x required");
+  if (sp.want_y && (!parts->y_hi || !parts->y_lo || !acc->y)) return fail(PDP_ERR_INVALID_ARG, "y required");
+  if (P == 0) return 0;
+  if (acc->row_count != parts->row_count)
+    HIP_TRY(hipMemcpyAsync(acc->row_count, parts->row_count, (size_t)P * 8, hipMemcpyDeviceToDevice, stream));
+  if (sp.want_count && acc->count != parts->count)
+    HIP_TRY(hipMemcpyAsync(acc->count, parts->count, (size_t)P * 8, hipMemcpyDeviceToDevice, stream));
+  // the exponents K4 used: k4_plan depends on the bounds and metrics only (n < 2^32 for partials)
+  const K4Plan k4 = k4_plan(bp, sp, 1, std::max<int64_t>(P, 1), false);
+  if (!k4.on) return fail(PDP_ERR_INVALID_ARG, "partials need the K4 reduction (PDP_K4 on)");
+  const unsigned grid = (unsigned)grid_for(P, kThreads, 4096);
+  if (sp.xmode != kXNone)
+    hipLaunchKernelGGL(k4_partials_to_double, dim3(grid), dim3(kThreads), 0, stream, (const long long*)parts->x_hi,
+                       (const long long*)parts->x_lo, (const unsigned long long*)parts->nan, 0,
+                       k4_red(k4, sp, P, false), acc->x, P);
+  if (sp.want_y)
+    hipLaunchKernelGGL(k4_partials_to_double, dim3(grid), dim3(kThreads), 0, stream, (const long long*)parts->y_hi,
+                       (const long long*)parts->y_lo, (const unsigned long long*)parts->nan, 32,
+                       k4_red(k4, sp, P, true), acc->y, P);
+  HIP_TRY(hipGetLastError());
+  return 0;
+}
+
 int pdp_bound_accumulate_sweep(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bps, int32_t num_configs,
                                const pdp_accumulators* accs, void* workspace, size_t workspace_bytes, void* stream) {
   return bound_impl(ctx, cols, bps, num_configs, accs, workspace, workspace_bytes, stream, true);
@@ -3128,6 +3289,7 @@ int pdp_utility_aggregate(pdp_ctx* ctx, const double* metrics, const double* pro
   AggParams prm{};
   prm.privacy_ids = privacy_ids;
   prm.P = P;
+  prm.nrows = nrows;
   const int nblocks = (int)std::max<int64_t>(1, std::min<int64_t>((P + kAggThreads - 1) / kAggThreads, kAggMaxBlocks));
   AsyncFrees scratch(stream);
   AggRow* d_rows = nullptr;
@@ -3138,7 +3300,8 @@ int pdp_utility_aggregate(pdp_ctx* ctx, const double* metrics, const double* pro
   prm.rows = d_rows;
   {
     ProfScope ps(ctx, PDP_STAGE_ANALYSIS_AGGREGATE, stream);
-    hipLaunchKernelGGL(k_agg_partials, dim3((unsigned)nblocks, (unsigned)nrows), dim3(kAggThreads), 0, stream, prm,
+    hipLaunchKernelGGL(k_agg_partials, dim3((unsigned)nblocks, (unsigned)std::min(nrows, 65535)), dim3(kAggThreads), 0,
+                       stream, prm,
                        partials);
     const int tot = nrows * kAggFields;
     hipLaunchKernelGGL(k_agg_final, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, stream, partials, d_rows, nrows,
@@ -3259,12 +3422,24 @@ int pdp_stream_copy(const void* src, void* dst, int64_t bytes, void* stream) {
   if (bytes < 0 || (bytes & 15) || (bytes && (!src || !dst))) return fail(PDP_ERR_INVALID_ARG, "bad copy args");
   if (bytes == 0) return 0;
   // default: non-temporal, 8 x 16 B in flight per lane, 32768 blocks (5.32 TB/s against 5.11 for the plain
-  // 4-deep form on the same box, tools/copy_probe.py)
+  // 4-deep form on the same box, tools/copy_probe.py).  PDP_COPY_VARIANT: 0 plain 4-deep; 1 nt loads + nt
+  // stores; 2 nt loads, default stores; 3 default loads + stores; 4 default loads, nt stores (8-deep);
+  // 5 read only (nt), 6 read only (default); 7 write only (nt), 8 write only (default) -- for 5-8 `bytes`
+  // is the bytes read or written
   const int variant = env_int("PDP_COPY_VARIANT", 1);
   const unsigned grid = (unsigned)env_int("PDP_COPY_GRID", 32768);
-  if (variant == 1)
-    hipLaunchKernelGGL(k_stream_copy_nt, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const u32x4*)src,
-                       (u32x4*)dst, bytes / 16);
+  auto kern = variant == 1 ? k_stream_copy_8<true, true, kCopyRW>
+            : variant == 2 ? k_stream_copy_8<true, false, kCopyRW>
+            : variant == 3 ? k_stream_copy_8<false, false, kCopyRW>
+            : variant == 4 ? k_stream_copy_8<false, true, kCopyRW>
+            : variant == 5 ? k_stream_copy_8<true, true, kCopyRead>
+            : variant == 6 ? k_stream_copy_8<false, false, kCopyRead>
+            : variant == 7 ? k_stream_copy_8<true, true, kCopyWrite>
+            : variant == 8 ? k_stream_copy_8<false, false, kCopyWrite>
+                           : nullptr;
+  if (kern)
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const u32x4*)src, (u32x4*)dst,
+                       bytes / 16);
   else
     hipLaunchKernelGGL(k_stream_copy, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const u32x4*)src, (u32x4*)dst,
                        bytes / 16);

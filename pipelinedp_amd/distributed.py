@@ -3,11 +3,16 @@
 Bounding is per privacy id, so once every row of a privacy id lives on one
 rank (rank = shard_of(pid)), contribution bounding is rank-local
 (contribution_bounders.py:87-92 groups by pid).  Each rank reduces its rows
-to dense per-partition accumulators over all P partitions; one reduce-scatter
-per accumulator array (int64 counts stay exact, fp64 sums differ only in
-summation order) leaves rank r with the sums of partition block
-[r*B, (r+1)*B); selection and noise run once there.  Philox counters use the
-global partition id, so released values do not depend on the rank count.
+to dense per-partition partials over all P partitions, with the sums in K4's
+exported 64-bit fixed point (pdp_bound_accumulate_partials); ONE int64 SUM
+reduce-scatter of all partial arrays leaves rank r with the exact integer
+sums of partition block [r*B, (r+1)*B), which are converted to fp64 once
+there (pdp_finalize_partials).  Counts AND sums are therefore identical bit
+for bit to a one-GPU run, whatever the world size or the collective's
+reduction order (the fixed-order merge of combine_accumulators_per_key,
+pipeline_backend.py:528-538).  Selection and noise run once on the owner;
+Philox counters use the global partition id, so released values do not
+depend on the rank count either.
 
 The collective backend is whatever ``torch.distributed`` was initialised
 with: ``nccl`` (= RCCL over xGMI on MI355X) for GPUs, ``gloo`` in CPU tests.
@@ -89,25 +94,26 @@ class World:
 
         return move(spid), move(spk), move(sval)
 
-    def reduce_scatter_accumulators(self, acc, num_partitions: int):
-        """Sums per-rank dense accumulators; returns owned-block tensors
-        [row_count, count, x, y] (None where absent)."""
+    def reduce_scatter_partials(self, parts, num_partitions: int):
+        """Sums the ranks' fixed-point partials (int64, exact) and returns the
+        owned block's as an executor.Partials of B = padded / size partitions.
+        One collective for all arrays: the [K, padded] partials are laid out
+        as [size, K, B] so that reduce_scatter_tensor hands rank r its
+        [K, B] slice."""
         import torch
         import torch.distributed as dist
+
+        from .executor import Partials
         _, _, padded = self.block(num_partitions)
         b = padded // self.size
-        outs = []
-        for t in (acc.row_count, acc.count, acc.x, acc.y):
-            if t is None:
-                outs.append(None)
-                continue
-            src = t[:num_partitions]
-            if padded != num_partitions:
-                src = torch.cat([src, src.new_zeros(padded - num_partitions)])
-            dst = src.new_empty(b)
-            dist.reduce_scatter_tensor(dst, src.contiguous(), op=dist.ReduceOp.SUM, group=self.group)
-            outs.append(dst)
-        return outs
+        data = parts.data[:, :num_partitions]
+        k = data.shape[0]
+        if padded != num_partitions:
+            data = torch.cat([data, data.new_zeros((k, padded - num_partitions))], dim=1)
+        src = data.reshape(k, self.size, b).permute(1, 0, 2).reshape(-1)  # [size * K * B], rank-major
+        dst = src.new_empty(k * b)
+        dist.reduce_scatter_tensor(dst, src, op=dist.ReduceOp.SUM, group=self.group)
+        return Partials(dst.view(k, b), parts.fields, b)
 
     def aggregate(self, ex, pid, pk, value, num_privacy_ids, num_partitions, bounds, rel, gather=True,
                   shuffle=False):
@@ -121,10 +127,10 @@ class World:
         import torch.distributed as dist
         if shuffle and pid is not None:
             pid, pk, value = self.shuffle_by_privacy_id(ex, pid, pk, value)
-        acc = ex.accumulate(pid, pk, value, num_privacy_ids, num_partitions, bounds)
+        parts = ex.accumulate_partials(pid, pk, value, num_privacy_ids, num_partitions, bounds)
         off, length, padded = self.block(num_partitions)
-        owned = self.reduce_scatter_accumulators(acc, num_partitions)
-        block_acc = _BlockAcc(owned, padded // self.size)
+        owned = self.reduce_scatter_partials(parts, num_partitions)
+        block_acc = ex.finalize_partials(owned, bounds)
         keep, out, fields = ex.release(block_acc, rel, bounds, pk_offset=off, num_partitions=padded // self.size)
         if not gather:
             return keep[:length], out[:, :length], fields
@@ -137,23 +143,6 @@ class World:
         dist.all_gather_into_tensor(out_all, out[:, :b].contiguous(), group=self.group)
         out_all = out_all.reshape(self.size, f, b).permute(1, 0, 2).reshape(f, padded)
         return keep_all[:num_partitions], out_all[:, :num_partitions], fields
-
-
-class _BlockAcc:
-    """Accumulators view of the owned block (duck-types executor.Accumulators)."""
-
-    def __init__(self, tensors, num_partitions):
-        self.row_count, self.count, self.x, self.y = tensors
-        self.num_partitions = num_partitions
-
-    def as_struct(self, offset: int = 0):
-        import ctypes
-        from . import native
-
-        def p(t):
-            return ctypes.c_void_p(t.data_ptr() + 8 * offset) if t is not None else None
-
-        return native.Accumulators(p(self.row_count), p(self.count), p(self.x), p(self.y))
 
 
 def _has_gpu():

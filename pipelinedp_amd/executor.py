@@ -74,6 +74,42 @@ class Accumulators:
         return native.Accumulators(p(self.row_count), p(self.count), p(self.x), p(self.y))
 
 
+class Partials:
+    """Per-partition partials in K4's exported 64-bit fixed point
+    (pdp_bound_accumulate_partials): one int64 tensor ``data`` [K, P] whose
+    rows are ``fields`` (row_count, count, x_hi, x_lo, y_hi, y_lo, nan as the
+    metrics need them).  Partials of several ranks add up exactly (an int64
+    SUM), and finalize() converts the sum once."""
+
+    def __init__(self, data, fields, num_partitions: int):
+        self.data = data
+        self.fields = list(fields)
+        self.num_partitions = int(num_partitions)
+
+    @staticmethod
+    def fields_for(metrics_mask: int):
+        m = metrics_mask
+        f = ["row_count"]
+        if m & (native.METRIC_COUNT | native.METRIC_MEAN | native.METRIC_VARIANCE):
+            f.append("count")
+        if m & (native.METRIC_SUM | native.METRIC_MEAN | native.METRIC_VARIANCE):
+            f += ["x_hi", "x_lo", "nan"]
+        if m & native.METRIC_VARIANCE:
+            f += ["y_hi", "y_lo"]
+        return f
+
+    def row(self, name):
+        return self.data[self.fields.index(name)] if name in self.fields else None
+
+    def as_struct(self) -> native.Partials:
+
+        def p(name):
+            t = self.row(name)
+            return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+        return native.Partials(p("row_count"), p("count"), p("x_hi"), p("x_lo"), p("y_hi"), p("y_lo"), p("nan"))
+
+
 class HipExecutor:
 
     def __init__(self, device=None):
@@ -140,6 +176,40 @@ class HipExecutor:
         native.check(self.lib.pdp_bound_accumulate(self.ctx, ctypes.byref(cols), ctypes.byref(bp), ctypes.byref(accs),
                                                    ctypes.c_void_p(ws.data_ptr()), ws.numel(), self.stream_handle),
                      "pdp_bound_accumulate")
+        return acc
+
+    def accumulate_partials(self, pid, pk, value, num_privacy_ids: int, num_partitions: int,
+                            cfg: BoundConfig) -> Partials:
+        """pdp_bound_accumulate_partials: the rank-local accumulate of the
+        multi-GPU path, sums in exported fixed point (see Partials)."""
+        cols = self._columns(pid, pk, value, num_privacy_ids, num_partitions)
+        bp = self._bound_params(cfg)
+        fields = Partials.fields_for(cfg.metrics_mask)
+        P = max(int(num_partitions), 1)
+        parts = Partials(self.torch.empty((len(fields), P), dtype=self.torch.int64, device=self.device), fields,
+                         num_partitions)
+        nbytes = ctypes.c_size_t(0)
+        native.check(self.lib.pdp_workspace_size(ctypes.byref(cols), ctypes.byref(bp), ctypes.byref(nbytes)),
+                     "pdp_workspace_size")
+        ws = self._workspace(nbytes.value)
+        ps = parts.as_struct()
+        native.check(self.lib.pdp_bound_accumulate_partials(self.ctx, ctypes.byref(cols), ctypes.byref(bp),
+                                                            ctypes.byref(ps), ctypes.c_void_p(ws.data_ptr()),
+                                                            ws.numel(), self.stream_handle),
+                     "pdp_bound_accumulate_partials")
+        return parts
+
+    def finalize_partials(self, parts: Partials, cfg: BoundConfig) -> Accumulators:
+        """pdp_finalize_partials: (summed) partials -> Accumulators for release."""
+        P = parts.num_partitions
+        acc = Accumulators(self.torch, P, self.device, cfg.metrics_mask)
+        acc.row_count = parts.row("row_count")
+        if acc.count is not None:
+            acc.count = parts.row("count")
+        bp = self._bound_params(cfg)
+        ps, accs = parts.as_struct(), acc.as_struct()
+        native.check(self.lib.pdp_finalize_partials(self.ctx, ctypes.byref(ps), P, ctypes.byref(bp),
+                                                    ctypes.byref(accs), self.stream_handle), "pdp_finalize_partials")
         return acc
 
     def accumulate_sweep(self, pid, pk, value, num_privacy_ids: int, num_partitions: int,

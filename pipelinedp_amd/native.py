@@ -40,6 +40,11 @@ class Accumulators(ctypes.Structure):
     _fields_ = [("row_count", c_vp), ("count", c_vp), ("x", c_vp), ("y", c_vp)]
 
 
+class Partials(ctypes.Structure):
+    _fields_ = [("row_count", c_vp), ("count", c_vp), ("x_hi", c_vp), ("x_lo", c_vp), ("y_hi", c_vp),
+                ("y_lo", c_vp), ("nan", c_vp)]
+
+
 class ReleaseParams(ctypes.Structure):
     _fields_ = [("metrics", c_i32), ("noise_kind", c_i32), ("selection", c_i32), ("add_noise", c_i32),
                 ("max_partitions_contributed", c_i64), ("max_contributions_per_partition", c_i64),
@@ -95,6 +100,10 @@ SIGNATURES = [
                                    ctypes.POINTER(ctypes.c_size_t)]),
     ("pdp_bound_accumulate", c_i32, [c_vp, ctypes.POINTER(Columns), ctypes.POINTER(BoundParams),
                                      ctypes.POINTER(Accumulators), c_vp, ctypes.c_size_t, c_vp]),
+    ("pdp_bound_accumulate_partials", c_i32, [c_vp, ctypes.POINTER(Columns), ctypes.POINTER(BoundParams),
+                                              ctypes.POINTER(Partials), c_vp, ctypes.c_size_t, c_vp]),
+    ("pdp_finalize_partials", c_i32, [c_vp, ctypes.POINTER(Partials), c_i64, ctypes.POINTER(BoundParams),
+                                      ctypes.POINTER(Accumulators), c_vp]),
     ("pdp_sweep_workspace_size", c_i32, [ctypes.POINTER(Columns), ctypes.POINTER(ctypes.c_size_t)]),
     ("pdp_bound_accumulate_sweep", c_i32, [c_vp, ctypes.POINTER(Columns), ctypes.POINTER(BoundParams), c_i32,
                                            ctypes.POINTER(Accumulators), c_vp, ctypes.c_size_t, c_vp]),

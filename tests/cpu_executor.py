@@ -51,7 +51,46 @@ class CpuExecutor:
         acc = o.bound_and_accumulate(None if pid is None else pid.numpy(), pk.numpy(),
                                      None if value is None else value.numpy(), num_partitions, _bound_params(cfg),
                                      "hash", seed=cfg.sampling_seed or 0)
+        # the per-partition merge in K4's fixed point, as the GPU sums (pdp_reduce.inc)
+        bp, m = _bound_params(cfg), cfg.metrics_mask
+        x, y = o.k4_finalize(o.k4_partials(acc, num_partitions, bp, m), bp, m)
+        if x is not None:
+            if m & (native.METRIC_MEAN | native.METRIC_VARIANCE):
+                acc.nsum = x
+            else:
+                acc.sum = x
+        if y is not None:
+            acc.nsumsq = y
         return _Acc(self.torch, acc, cfg.metrics_mask, num_partitions)
+
+    def accumulate_partials(self, pid, pk, value, num_privacy_ids, num_partitions, cfg):
+        """pdp_bound_accumulate_partials restated: the oracle's kept pairs in
+        K4's exported fixed point (pdp_oracle.k4_partials)."""
+        from pipelinedp_amd.executor import Partials
+        self.calls.append(("accumulate", int(pk.numel())))
+        acc = o.bound_and_accumulate(None if pid is None else pid.numpy(), pk.numpy(),
+                                     None if value is None else value.numpy(), num_partitions, _bound_params(cfg),
+                                     "hash", seed=cfg.sampling_seed or 0)
+        parts = o.k4_partials(acc, num_partitions, _bound_params(cfg), cfg.metrics_mask)
+        fields = Partials.fields_for(cfg.metrics_mask)
+        return Partials(self.torch.from_numpy(np.stack([parts[f] for f in fields])), fields, num_partitions)
+
+    def finalize_partials(self, parts, cfg):
+        """pdp_finalize_partials restated (pdp_oracle.k4_finalize)."""
+        torch = self.torch
+        d = {f: parts.row(f).numpy() for f in parts.fields}
+        x, y = o.k4_finalize(d, _bound_params(cfg), cfg.metrics_mask)
+
+        class A:
+            pass
+
+        a = A()
+        a.num_partitions = parts.num_partitions
+        a.row_count = parts.row("row_count")
+        a.count = parts.row("count")
+        a.x = None if x is None else torch.from_numpy(x)
+        a.y = None if y is None else torch.from_numpy(y)
+        return a
 
     def release(self, acc, cfg, bounds, pk_offset=0, num_partitions=None):
         torch = self.torch

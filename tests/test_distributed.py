@@ -2,14 +2,16 @@
 gloo on 127.0.0.1, the same World.aggregate code the RCCL bench runs.
 
 Each rank bounds/accumulates only the rows of its privacy ids (rank =
-shard_of(pid)), the dense partials are reduce-scattered, the owned partition
-block is released with global partition ids, and the blocks are
-all-gathered.  The per-rank compute is the CPU oracle (test-only stand-in
-for HipExecutor, same accumulate/release interface): what is under test is
-the sharding, the collectives and the block bookkeeping.  Expected result:
-one single-process oracle run over all rows.  Counts, privacy-id counts and
-keep decisions bit-exact; fp64 sums to 1e-9 relative (summation order);
-noisy outputs with identical Philox draws to 1e-9.
+shard_of(pid)), the dense fixed-point partials are reduce-scattered as int64,
+converted once on the owner, the owned partition block is released with
+global partition ids, and the blocks are all-gathered.  The per-rank compute
+is the CPU oracle (test-only stand-in for HipExecutor, same
+accumulate_partials / finalize_partials / release interface, K4's fixed
+point restated in pdp_oracle.k4_partials): what is under test is the
+sharding, the collectives and the block bookkeeping.  Expected result: one
+single-process run over all rows with the same fixed-point merge --
+everything bit for bit, sums and noisy outputs included, because integer
+partial sums do not depend on how the pairs are split over ranks.
 """
 import os
 import socket
@@ -30,23 +32,42 @@ def _rows():
     return o.synth_rows(N, U, P, seed=17, zipf_s=1.1)
 
 
-class OracleExecutor:
-    """accumulate / release with HipExecutor's signatures, computed by the
-    CPU oracle on torch CPU tensors (test infrastructure only)."""
+MASK = 1 | 2 | 4 | 16
 
-    def accumulate(self, pid, pk, value, num_privacy_ids, num_partitions, bounds):
+
+def _single_process_fixed(pid, pk, val):
+    """One process over all rows, sums merged in K4's fixed point."""
+    acc = o.bound_and_accumulate(pid, pk, val, P, BP, "hash", seed=5)
+    x, _ = o.k4_finalize(o.k4_partials(acc, P, BP, MASK), BP, MASK)
+    acc.nsum = x
+    return acc
+
+
+class OracleExecutor:
+    """accumulate_partials / finalize_partials / release with HipExecutor's
+    signatures, computed by the CPU oracle on torch CPU tensors (test
+    infrastructure only)."""
+
+    def accumulate_partials(self, pid, pk, value, num_privacy_ids, num_partitions, bounds):
         import torch
+
+        from pipelinedp_amd.executor import Partials
         acc = o.bound_and_accumulate(pid.numpy(), pk.numpy(), value.numpy(), num_partitions, BP, "hash", seed=5)
+        parts = o.k4_partials(acc, num_partitions, BP, MASK)
+        fields = Partials.fields_for(MASK)
+        return Partials(torch.from_numpy(np.stack([parts[f] for f in fields])), fields, num_partitions)
+
+    def finalize_partials(self, parts, bounds):
+        import torch
+        x, _ = o.k4_finalize({f: parts.row(f).numpy() for f in parts.fields}, BP, MASK)
 
         class A:
             pass
 
         a = A()
-        a.num_partitions = num_partitions
-        a.row_count = torch.from_numpy(acc.row_count.astype(np.int64))
-        a.count = torch.from_numpy(acc.count.astype(np.int64))
-        a.x = torch.from_numpy(acc.nsum.astype(np.float64))
-        a.y = None
+        a.num_partitions = parts.num_partitions
+        a.row_count, a.count = parts.row("row_count"), parts.row("count")
+        a.x, a.y = torch.from_numpy(x), None
         return a
 
     def release(self, acc, rel, bounds, pk_offset=0, num_partitions=None):
@@ -71,11 +92,13 @@ def _worker(rank, world_size, port, outdir):
         w = World(rank, world_size)
         t = lambda a: torch.from_numpy(np.ascontiguousarray(a[mine]))  # noqa: E731
         keep, out, fields = w.aggregate(OracleExecutor(), t(pid), t(pk), t(val), U, P, None, None, gather=True)
-        acc = OracleExecutor().accumulate(t(pid), t(pk), t(val), U, P, None)
-        owned = w.reduce_scatter_accumulators(acc, P)
+        parts = OracleExecutor().accumulate_partials(t(pid), t(pk), t(val), U, P, None)
+        owned = w.reduce_scatter_partials(parts, P)
+        x = OracleExecutor().finalize_partials(owned, None).x
         off, length, _ = w.block(P)
         np.savez(os.path.join(outdir, f"rank{rank}.npz"), keep=keep.numpy(), out=out.numpy(),
-                 rows=np.int64(mine.sum()), off=off, length=length, row_count=owned[0].numpy()[:length])
+                 rows=np.int64(mine.sum()), off=off, length=length, row_count=owned.row("row_count").numpy()[:length],
+                 x=x.numpy()[:length])
     finally:
         dist.destroy_process_group()
 
@@ -123,16 +146,20 @@ def test_two_ranks_shard_all_rows(two_rank_run):
 
 def test_two_ranks_match_single_process(two_rank_run):
     pid, pk, val = _rows()
-    acc = o.bound_and_accumulate(pid, pk, val, P, BP, "hash", seed=5)
+    acc = _single_process_fixed(pid, pk, val)
     keep, out = o.release(acc, BP, SPEC, seed=9)
     for r in two_rank_run:  # every rank holds the gathered result
         assert np.array_equal(r["keep"].astype(bool), keep)
         for i, f in enumerate(FIELDS):
-            np.testing.assert_allclose(r["out"][i], out[f], rtol=1e-9, atol=1e-9, err_msg=f)
-    # the reduce-scattered privacy-id counts are exact on each owned block
+            np.testing.assert_array_equal(r["out"][i], out[f], err_msg=f)
+    # the reduce-scattered privacy-id counts and the converted sums are exact on each owned block
     for r in two_rank_run:
         off, ln = int(r["off"]), int(r["length"])
         assert np.array_equal(r["row_count"], acc.row_count[off:off + ln])
+        np.testing.assert_array_equal(r["x"], acc.nsum[off:off + ln])
+    # and the fixed-point sums are the fp64 sums to 1e-12 (per-pair rounding 2^-63 max|x|)
+    ref = o.bound_and_accumulate(pid, pk, val, P, BP, "hash", seed=5)
+    np.testing.assert_allclose(acc.nsum, ref.nsum, rtol=1e-12, atol=1e-9)
 
 
 # --- DPEngine.aggregate with a 2-rank world (gloo) ---------------------------
@@ -204,7 +231,7 @@ def test_dp_engine_two_ranks_matches_one_process(engine_two_ranks):
         got = [(k, tuple(v)) for k, v in r["out"]]
         assert [k for k, _ in got] == [k for k, _ in want]
         for (_, g), (_, w) in zip(got, want):
-            np.testing.assert_allclose(g, w, rtol=1e-9, atol=1e-9)
+            np.testing.assert_array_equal(g, w)
 
 
 def test_dp_engine_two_ranks_shuffle_moves_rows_by_privacy_id(engine_two_ranks):

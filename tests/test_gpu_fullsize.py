@@ -141,6 +141,77 @@ def test_c3_release_selection_and_noise_full_size(ex):
     assert abs(np.mean(np.abs(resid)) - bscale) <= 5 * bscale / math.sqrt(P)
 
 
+def test_c3_variance_full_size(ex):
+    """c3 as BASELINE.json configs[2] defines it: MEAN + VARIANCE (+ COUNT +
+    SUM) at 1e9 rows, 1e7 privacy ids, 1e6 Zipf(1.1) partitions, L0 = 4,
+    Linf = 2, [0, 10], truncated-geometric selection.  This runs the VARIANCE
+    slot array and K4's second (y) run at full size.
+
+    * the L0 pre-filter is exact: filtered == unfiltered bit for bit for
+      row_count, count, x AND y (K4 sums in fixed point, so the record order
+      of the two paths does not matter);
+    * 0 <= y <= count * ((b - a) / 2)^2 (VarianceCombiner.create_accumulator,
+      combiners.py:371-381: y = sum of (clip(v) - mid)^2);
+    * noise-off release equals compute_dp_var's formulas on the accumulators
+      (dp_computations.py:400-459 with _compute_mean_for_normalized_sum
+      :310-345): mean_sq = y / max(1, count), var = mean_sq - (x / max(1,
+      count))^2, mean = x / max(1, count) + mid, sum = mean * count."""
+    import torch
+
+    from pipelinedp_amd import native
+    from pipelinedp_amd.executor import BoundConfig, ReleaseConfig
+    n, U, P, L0, Linf, a, b = 1_000_000_000, 10_000_000, 1_000_000, 4, 2, 0.0, 10.0
+    mask = MASK_COUNT | MASK_SUM | MASK_MEAN | native.METRIC_VARIANCE
+    pid, pk, val = ex.generate(n, U, P, seed=20250204, zipf_s=1.1, lo=a, hi=b)
+    cfg = BoundConfig(mask, L0, Linf, a, b, sampling_seed=13)
+    acc = ex.accumulate(pid, pk, val, U, P, cfg)
+    torch.cuda.synchronize()
+    assert 0 < ex.stats().filter_rows < n // 5  # the pre-filter ran
+    rc, cnt, x, y = acc.row_count.clone(), acc.count.clone(), acc.x.clone(), acc.y.clone()
+    del acc
+    nofilter = BoundConfig(mask, L0, Linf, a, b, sampling_seed=13, debug_flags=NO_FILTER)
+    acc2 = ex.accumulate(pid, pk, val, U, P, nofilter)
+    torch.cuda.synchronize()
+    assert ex.stats().filter_rows == 0
+    assert torch.equal(acc2.row_count, rc)
+    assert torch.equal(acc2.count, cnt)
+    assert torch.equal(acc2.x, x)
+    assert torch.equal(acc2.y, y)
+    del acc2, pid, pk, val
+
+    half = (b - a) / 2
+    cf = cnt.to(torch.float64)
+    assert int(rc.sum()) > 0
+    assert bool((y >= 0).all()) and bool((y <= cf * half * half * (1 + 1e-12) + 1e-9).all())
+    assert bool((x.abs() <= cf * half + 1e-6).all())
+    assert bool((x * x <= y * cf * (1 + 1e-9) + 1e-6).all())  # Cauchy-Schwarz on the kept terms
+
+    eps = [0.0, 0.0, 0.0, 0.5, 0.0, 0.5]
+    delta = [0.0] * 5 + [1e-6]
+    from pipelinedp_amd.executor import Accumulators
+    acc = Accumulators(torch, P, rc.device, mask)
+    acc.row_count.copy_(rc)
+    acc.count.copy_(cnt)
+    acc.x.copy_(x)
+    acc.y.copy_(y)
+    off = ReleaseConfig(mask, native.NOISE_LAPLACE, native.SELECTION_TRUNCATED_GEOMETRIC, eps, delta, 1,
+                        add_noise=False, noise_seed=3)
+    keep, out, fields = ex.release(acc, off, cfg)
+    torch.cuda.synchronize()
+    assert sorted(fields) == ["count", "mean", "sum", "variance"]
+    f = {name: out[i] for i, name in enumerate(fields)}
+    den = cf.clamp(min=1.0)
+    nmean = x / den
+    var = y / den - nmean * nmean
+    mean = nmean + (a + half)
+    assert torch.equal(f["count"], cf)
+    tol = lambda v: 1e-12 * v.abs().clamp(min=1.0)  # noqa: E731  (division order only)
+    assert bool(((f["mean"] - mean).abs() <= tol(mean)).all())
+    assert bool(((f["variance"] - var).abs() <= tol(var) + 1e-12 * half * half).all())
+    assert bool(((f["sum"] - mean * cf).abs() <= tol(mean * cf)).all())
+    assert torch.equal(keep.bool(), rc > 0)  # noise-free: keep iff p(n) > 0
+
+
 def test_c4_shard_binding_invariants(ex):
     """c4 shard (BASELINE configs[3] per GPU): 5e8 rows, 1.25e7 privacy ids,
     5e7 Zipf(1.1) partitions, L0=32, Linf=4 -- the LDS partition cache under

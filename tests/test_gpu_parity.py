@@ -79,6 +79,7 @@ CONFIGS = [
     (12000, 200, 500, 1.1, 70, 1, (0.0, 10.0), None, 1 | 2 | 16),  # sorted K2 with two output slots
     (40000, 300, 500, 1.1, 3, 12, (0.0, 10.0), None, 1 | 2 | 4 | 8 | 16),  # pre-filter with L_inf > 8: k_lean
     (60000, 150, 2000, 1.2, 8, 8, (-1.0, 6.0), (-2.0, 30.0), 1 | 2),  # largest thin L0 / L_inf, sum bounds
+    (30000, 2, 3, 0.0, 2, 4, (0.0, 10.0), None, 1 | 2 | 4 | 8 | 16),  # (pid, pk) groups of ~5000 rows: big-group kernel
 ]
 
 
@@ -554,3 +555,35 @@ def test_select_partitions_binding_matches_reference_distribution_on_gpu(ex):
     p = (freq + d["freq"]) / 2
     sd = np.sqrt(2 * p * (1 - p) / runs) + 1e-9
     assert np.all(np.abs(freq - d["freq"]) <= 4.5 * sd), (freq, d["freq"])
+
+
+def test_heavy_single_group_generic_path(ex):
+    """one privacy id with 2e6 rows in ONE partition (plus a
+    spread of ordinary rows) goes through the generic path, whose kept groups
+    of more than 2048 rows are summed by a whole block (k_stream_big_groups)
+    instead of one lane walking every row.  Counts bit-exact against the
+    oracle, sums to 1e-9; the accumulate call stays well under the time a
+    single-lane walk of 2e6 rows takes."""
+    import time
+
+    import torch
+    n0, U, P = 200000, 3000, 500
+    pid0, pk0, val0 = o.synth_rows(n0, U, P, seed=4242, zipf_s=1.1, value_lo=-5, value_hi=15)
+    heavy = 2_000_000
+    rng = np.random.default_rng(7)
+    pid = np.concatenate([pid0, np.full(heavy, U, np.int64), np.full(300, U, np.int64)])
+    pk = np.concatenate([pk0, np.full(heavy, 17, np.int64), rng.integers(0, P, 300)])
+    val = np.concatenate([val0, rng.uniform(-5, 15, heavy), rng.uniform(-5, 15, 300)])
+    perm = rng.permutation(len(pid))
+    pid, pk, val = pid[perm], pk[perm], val[perm]
+    for L0, Linf in ((3, 2), (2, 5000)):
+        bp = o.BoundParams(L0, Linf, 0.0, 10.0)
+        mask = 1 | 2 | 4 | 8 | 16
+        run_gpu(ex, pid, pk, val, U + 1, P, bp, mask, seed=5)  # warm-up
+        t0 = time.perf_counter()
+        _, _, rc, cnt, x, y = run_gpu(ex, pid, pk, val, U + 1, P, bp, mask, seed=5)
+        dt = time.perf_counter() - t0
+        assert ex.stats().fallback_rows >= heavy
+        ref = o.bound_and_accumulate(pid, pk, val, P, bp, "hash", seed=5)
+        check_acc(ref, rc, cnt, x, y, mask, val)
+        assert dt < 0.5, dt

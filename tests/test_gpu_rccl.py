@@ -109,3 +109,57 @@ def test_dp_engine_with_world_on_rccl_matches_single_process(rccl):
     assert [k for k, _ in got] == [k for k, _ in want]
     for (_, g), (_, w) in zip(got, want):
         np.testing.assert_array_equal(g, w)
+
+
+@pytest.mark.parametrize("world_size", [2, 3, 8])
+@pytest.mark.parametrize("metrics", ["mean_var", "sum_clip", "sum_partition_bounds"])
+def test_partials_over_emulated_ranks_equal_one_gpu_bitwise(world_size, metrics):
+    """The multi-GPU merge without a process group: the rows are split by
+    shard_of(pid) into world_size shards, each shard runs
+    pdp_bound_accumulate_partials on this GPU, the int64 partials are summed
+    (what the RCCL SUM reduce-scatter does, in any order), and
+    pdp_finalize_partials converts once.  Counts AND fp64 sums equal one
+    pdp_bound_accumulate over all rows bit for bit (K4's fixed point is an
+    integer sum), for MEAN + VARIANCE (x and y runs), clipped SUM and SUM with
+    per-partition sum bounds; a NaN value makes its partition's sums NaN on
+    both paths."""
+    import torch
+    from pipelinedp_amd import native
+    from pipelinedp_amd.distributed import shard_of
+    from pipelinedp_amd.executor import BoundConfig, HipExecutor, Partials
+    ex = HipExecutor(0)
+    n, U, P = 120000, 3000, 1500
+    pid, pk, val = o.synth_rows(n, U, P, seed=31, zipf_s=1.1, value_lo=-5, value_hi=15)
+    # one more privacy id with a single NaN row in partition 5: always kept
+    pid, pk, val = np.append(pid, U), np.append(pk, 5), np.append(val, np.nan)
+    U += 1
+    M = native
+    if metrics == "mean_var":
+        cfg = BoundConfig(M.METRIC_COUNT | M.METRIC_MEAN | M.METRIC_VARIANCE | M.METRIC_PRIVACY_ID_COUNT, 3, 4,
+                          0.0, 10.0, sampling_seed=12)
+    elif metrics == "sum_clip":
+        cfg = BoundConfig(M.METRIC_COUNT | M.METRIC_SUM, 4, 3, -2.0, 12.0, sampling_seed=12)
+    else:
+        cfg = BoundConfig(M.METRIC_SUM, 5, 2, None, None, -3.0, 25.0, sampling_seed=12)
+    d = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
+    one = ex.accumulate(d(pid), d(pk), d(val), U, P, cfg)
+    shard = shard_of(pid, world_size)
+    total = None
+    for r in range(world_size):
+        m = shard == r
+        parts = ex.accumulate_partials(d(pid[m]), d(pk[m]), d(val[m]), U, P, cfg)
+        total = parts.data.clone() if total is None else total + parts.data
+    acc = ex.finalize_partials(Partials(total, parts.fields, P), cfg)
+    torch.cuda.synchronize()
+    for name in ("row_count", "count"):
+        a, b = getattr(one, name), getattr(acc, name)
+        assert (a is None) == (b is None)
+        if a is not None:
+            assert torch.equal(a, b), name
+    for name in ("x", "y"):
+        a, b = getattr(one, name), getattr(acc, name)
+        assert (a is None) == (b is None)
+        if a is not None:
+            np.testing.assert_array_equal(a.cpu().numpy(), b.cpu().numpy(), err_msg=name)
+    if one.x is not None:
+        assert bool(torch.isnan(one.x[5])) and int(torch.isnan(one.x).sum()) == 1
