@@ -45,10 +45,14 @@ constexpr int kThreads = 256;
 #define PDP_OS_STAGE_DIV 2
 #endif
 constexpr int kItems = PDP_OS_ITEMS;         // rows per thread in a radix tile
-constexpr int kTile = kThreads * kItems;     // 4096 rows per radix tile
-// Other tile sizes are not supported: a 12-rows-per-thread build (3072-row
-// tiles) faulted on the GPU in the pre-filter path (round-3 experiment).
-static_assert(kTile == 4096, "the radix / filter kernels assume 4096-row tiles");
+constexpr int kTile = kThreads * kItems;     // 4096 rows per radix tile (16 rows per thread)
+// Round 3's 12-rows-per-thread build (3072-row tiles) faulted: the per-tile
+// count loops stepped over the items in groups of kHistUnroll = 8 rows per
+// thread (items 0-7, 8-15) without stopping at kItems = 12, so every tile's
+// digit counts also took 1024 rows of the NEXT tile; the tile bases then
+// overran the record buffer in the bucket pass's scatter.  The record-pass
+// loads had the same overrun (groups of kRecGroup = 16 past r[12]).  Every
+// grouped item loop is now bounded by kItems.
 constexpr int kMaxPasses = 12;
 constexpr int kHist = 257;                   // 256 digits + drop bucket
 constexpr int kStatusStride = 256;
@@ -174,6 +178,7 @@ constexpr int kDebugSweepStamps = 8192;  // per-phase cycle stamps in k_onesweep
 constexpr int kDebugSortOnly = 16384;
 constexpr int kDebugNoLookback = 32768;
 constexpr int kDebugLinearWrite = 65536;
+constexpr int kDebugNoScatter = 2048;  // with kDebugSortOnly: the radix passes stage in LDS but store nothing
 constexpr int kDebugLookback = 131072;  // radix passes by decoupled look-back instead of reduce-then-scan
 constexpr int kDebugNoAtomics = 262144;  // K2 skips its accumulator atomics (timing ablation)
 constexpr int kDebugNoHotCache = 524288;  // k_lean emits straight to HBM (no LDS partition cache)
@@ -383,13 +388,13 @@ __global__ __launch_bounds__(kThreads) void k_histogram_tiles(const int64_t* __r
     for (int g = 0; g < kItems; g += kHistUnroll) {
       int64_t a[kHistUnroll], b[kHistUnroll];
 #pragma unroll
-      for (int u = 0; u < kHistUnroll; ++u) {  // loads first (clamped), then the counting
+      for (int u = 0; u < kHistUnroll && g + u < kItems; ++u) {  // loads first (clamped), then the counting
         const int64_t i = base + (int64_t)(g + u) * kThreads, ic = full || i < n ? i : n - 1;
         a[u] = pid[ic];
         b[u] = PID_ONLY ? 0 : pk[ic];
       }
 #pragma unroll
-      for (int u = 0; u < kHistUnroll; ++u) {
+      for (int u = 0; u < kHistUnroll && g + u < kItems; ++u) {
         if (!full && base + (int64_t)(g + u) * kThreads >= n) break;
         if (b[u] < 0 || b[u] >= (int64_t)ks.num_parts || a[u] < 0 || a[u] >= (int64_t)ks.num_pids) {
           if (b[u] >= 0) ++invalid;
@@ -436,12 +441,12 @@ __global__ __launch_bounds__(kThreads) void k_tile_counts(const Rec* __restrict_
     for (int g = 0; g < kItems; g += kHistUnroll) {
       Rec r[kHistUnroll];
 #pragma unroll
-      for (int u = 0; u < kHistUnroll; ++u) {
+      for (int u = 0; u < kHistUnroll && g + u < kItems; ++u) {
         const int64_t i = base + (int64_t)(g + u) * kThreads;
         if (n > 0) r[u] = rin[i < n ? i : n - 1];  // n == 0 (every row dropped): no load at all
       }
 #pragma unroll
-      for (int u = 0; u < kHistUnroll; ++u)
+      for (int u = 0; u < kHistUnroll && g + u < kItems; ++u)
         if (base + (int64_t)(g + u) * kThreads < n) atomicAdd(&st[digit_of(ks, pass, r[u])], 1u);
     }
     __syncthreads();
@@ -615,7 +620,7 @@ __device__ __forceinline__ void onesweep_body(
    for (int g = 0; g < kItems; g += kSoaGroup) {
     int64_t a[kItems], b[kItems];
 #pragma unroll
-    for (int k = g; k < g + kSoaGroup; ++k) {
+    for (int k = g; k < g + kSoaGroup && k < kItems; ++k) {
       const int64_t idx = base + k * 64;
       const int64_t ic = full ? idx : (idx < last ? idx : last);
       a[k] = pid[ic];
@@ -623,16 +628,16 @@ __device__ __forceinline__ void onesweep_body(
     }
     if (val) {
 #pragma unroll
-      for (int k = g; k < g + kSoaGroup; ++k) {
+      for (int k = g; k < g + kSoaGroup && k < kItems; ++k) {
         const int64_t idx = base + k * 64;
         r[k].val = val[full ? idx : (idx < last ? idx : last)];
       }
     } else {
 #pragma unroll
-      for (int k = g; k < g + kSoaGroup; ++k) r[k].val = 0.0;
+      for (int k = g; k < g + kSoaGroup && k < kItems; ++k) r[k].val = 0.0;
     }
 #pragma unroll
-    for (int k = g; k < g + kSoaGroup; ++k) {
+    for (int k = g; k < g + kSoaGroup && k < kItems; ++k) {
       uint32_t d;
       const bool valid = full || base + k * 64 <= last;
       r[k].pid = (uint32_t)a[k];
@@ -664,13 +669,13 @@ __device__ __forceinline__ void onesweep_body(
 #pragma unroll
    for (int g = 0; g < kItems; g += kRecGroup) {
 #pragma unroll
-    for (int k = g; k < g + kRecGroup; ++k) {
+    for (int k = g; k < g + kRecGroup && k < kItems; ++k) {
       const int64_t idx = base + k * 64;
       const int64_t ic = full ? idx : (idx < last ? idx : last);
       r[k] = ld_rec(ic < split ? rin + ic : rin2 + (ic - split));
     }
 #pragma unroll
-    for (int k = g; k < g + kRecGroup; ++k) {
+    for (int k = g; k < g + kRecGroup && k < kItems; ++k) {
       const uint32_t d = (ks.mode == 6 && r[k].pid == kK4EmptyKey) ? 256u : digit_of(ks, pass, r[k]);  // K4: empty slot
       dr[k] = (full || base + k * 64 <= last) ? d : 257u;
     }
@@ -845,7 +850,8 @@ __device__ __forceinline__ void onesweep_body(
       if (q < (uint32_t)kHalfTile) s_rec[q] = r[k];
     }
     __syncthreads();
-    const unsigned int e = tot - h < (unsigned int)kHalfTile ? tot - h : (unsigned int)kHalfTile;
+    const unsigned int e = (ks.ablate & kDebugNoScatter) ? 0u
+                           : tot - h < (unsigned int)kHalfTile ? tot - h : (unsigned int)kHalfTile;
     for (unsigned int i = t; i < e; i += kThreads) {
       const Rec rc = s_rec[i];
       if (ks.ablate & kDebugLinearWrite) {
@@ -2474,7 +2480,7 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
     }
   }
   ks.prof = (sp.debug & kDebugSweepStamps) != 0;
-  ks.ablate = (sp.debug & kDebugSortOnly) ? (sp.debug & (kDebugNoLookback | kDebugLinearWrite)) : 0;
+  ks.ablate = (sp.debug & kDebugSortOnly) ? (sp.debug & (kDebugNoLookback | kDebugLinearWrite | kDebugNoScatter)) : 0;
   const bool rts = use_tile_scan(n, sp.debug);
   const TileScan ts = rts ? tile_scan_bufs(ctx, status, L.tiles) : TileScan{};
   // L0 pre-filter (pdp_filter.inc): one pass on the bucket digit instead of the full pid sort
