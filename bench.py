@@ -494,8 +494,13 @@ def main():
     if roofline is not None:
         roofline["copy_peak_measured"] = copy_gbs
         roofline["copy_peak_note"] = ("pdp_stream_copy: non-temporal 16-B-per-lane streaming copy of 8 GiB (8 loads "
-                                      "in flight per lane), (read + write) bytes / time; the achievable ceiling next "
-                                      "to the 8 TB/s spec peak")
+                                      "in flight per lane, 32768 workgroups), (read + write) bytes / time -- the best "
+                                      "of the copy shapes tools/copy_probe.py sweeps (plain / nt loads and stores, "
+                                      "2048-32768 workgroups: 4.7-5.6 TB/s; a read-only stream reaches 7.1 TB/s, "
+                                      "profiles/r04_copy_probe.json); the achievable ceiling of a read+write kernel "
+                                      "next to the 8 TB/s spec peak")
+        if copy_gbs and roofline.get("unit") == "GB/s":
+            roofline["frac_of_copy"] = round(roofline["achieved"] / copy_gbs, 4)
     if rank == 0:
         e2e = rows_per_s * 24 / 1e9
         line = {

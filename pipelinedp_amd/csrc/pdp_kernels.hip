@@ -310,6 +310,9 @@ __device__ __forceinline__ T block_max(T v, T* s_tmp) {
 #ifndef PDP_HIST_UNROLL
 #define PDP_HIST_UNROLL 8
 #endif
+#ifndef PDP_HIST_NT
+#define PDP_HIST_NT 0  // non-temporal column loads in k_histogram_tiles
+#endif
 constexpr int kHistUnroll = PDP_HIST_UNROLL;  // rows per thread with loads in flight together (K0, K1u)
 
 template <bool SOA>
@@ -390,8 +393,13 @@ __global__ __launch_bounds__(kThreads) void k_histogram_tiles(const int64_t* __r
 #pragma unroll
       for (int u = 0; u < kHistUnroll && g + u < kItems; ++u) {  // loads first (clamped), then the counting
         const int64_t i = base + (int64_t)(g + u) * kThreads, ic = full || i < n ? i : n - 1;
+#if PDP_HIST_NT
+        a[u] = __builtin_nontemporal_load(pid + ic);
+        b[u] = PID_ONLY ? 0 : __builtin_nontemporal_load(pk + ic);
+#else
         a[u] = pid[ic];
         b[u] = PID_ONLY ? 0 : pk[ic];
+#endif
       }
 #pragma unroll
       for (int u = 0; u < kHistUnroll && g + u < kItems; ++u) {
@@ -539,10 +547,25 @@ constexpr int kLookback = PDP_LOOKBACK;
 // per-tile latency chain (tile claim, loads, look-back) is hidden by the
 // other blocks instead of idling the CU.
 constexpr int kHalfTile = kTile / PDP_OS_STAGE_DIV;
+// SoA rows loaded per batch (first pass / bucket pass).  All of a thread's rows at once (3 x 16 loads in
+// flight per lane, then the digits / tags): bucket pass 11.3 -> 8.9 ms against one row at a time (r04a,
+// same box; the no-scatter ablation put the old load phase at 8.2 ms of 11.3).
 #ifndef PDP_SOA_GROUP
-#define PDP_SOA_GROUP 1
+#define PDP_SOA_GROUP 16
 #endif
-constexpr int kSoaGroup = PDP_SOA_GROUP;  // SoA rows loaded per batch (first pass / bucket pass)
+constexpr int kSoaGroup = PDP_SOA_GROUP < kItems ? PDP_SOA_GROUP : kItems;
+// Non-temporal loads of the SoA input columns (read once per pass).
+#ifndef PDP_SOA_NT
+#define PDP_SOA_NT 0
+#endif
+template <typename T>
+__device__ __forceinline__ T ld_soa(const T* p) {
+#if PDP_SOA_NT
+  return __builtin_nontemporal_load(p);
+#else
+  return *p;
+#endif
+}
 #ifndef PDP_REC_GROUP
 #define PDP_REC_GROUP 16
 #endif
@@ -623,14 +646,14 @@ __device__ __forceinline__ void onesweep_body(
     for (int k = g; k < g + kSoaGroup && k < kItems; ++k) {
       const int64_t idx = base + k * 64;
       const int64_t ic = full ? idx : (idx < last ? idx : last);
-      a[k] = pid[ic];
-      b[k] = pk[ic];
+      a[k] = ld_soa(pid + ic);
+      b[k] = ld_soa(pk + ic);
     }
     if (val) {
 #pragma unroll
       for (int k = g; k < g + kSoaGroup && k < kItems; ++k) {
         const int64_t idx = base + k * 64;
-        r[k].val = val[full ? idx : (idx < last ? idx : last)];
+        r[k].val = ld_soa(val + (full ? idx : (idx < last ? idx : last)));
       }
     } else {
 #pragma unroll
@@ -2761,7 +2784,8 @@ int keep_table(int selection, double eps, double delta, int64_t k, std::vector<d
 }
 
 struct AnaLayout {
-  size_t recs_a, recs_b, flags, ppk, pref, pcnt, psum, npart, pbeg, mom, cfg, keep, hist, off, counters, status, total;
+  size_t recs_a, recs_b, flags, ppk, pref, pcnt, psum, npart, pbeg, mom, cfg, keep, hist, off, counters, status, slots,
+      total;
   AnaGroups groups{};  // distinct L0 values (G = 0: more than kAnaMaxGroups)
   int64_t tiles;
   std::vector<AnaCfg> cfgs;  // keep pointers are offsets until bound to the workspace
@@ -2827,6 +2851,9 @@ int ana_layout(int64_t n, int64_t U, int64_t P, const pdp_analysis_config* cfgs,
   L.counters = take(kNumCounters * 8);
   L.tiles = (int64_t)(n1 + kTile - 1) / kTile;
   L.status = take((size_t)L.tiles * kStatusStride * 8);
+  // k_ana_metrics' chunk-boundary partials: [chunk][head, tail][kAnaSlotFields][configurations / 64 * 64]
+  const size_t chunk = (size_t)kAnaChunk * (size_t)((nconf + 63) / 64);
+  L.slots = take((n1 + chunk - 1) / chunk * 2 * kAnaSlotFields * (size_t)((nconf + 63) / 64 * 64) * 8);
   L.total = o;
   return 0;
 }
@@ -2966,7 +2993,8 @@ int analysis_impl(pdp_ctx* ctx, const int64_t* pid, const int64_t* pk, const dou
                        cfg_d, nconf, mflags, P, out->metrics);
   const unsigned cgroups = (unsigned)((nconf + 63) / 64);
   if (M > 0) {
-    const int64_t waves = (M + kAnaChunk - 1) / kAnaChunk;
+    const int64_t chunk = (int64_t)kAnaChunk * cgroups;
+    const int64_t waves = (M + chunk - 1) / chunk;
     decltype(&k_ana_metrics<true, true, true>) km = nullptr;
     switch (mflags & (PDP_METRIC_SUM | PDP_METRIC_COUNT | PDP_METRIC_PRIVACY_ID_COUNT)) {
 #define PDP_KM(S, C, I)                                                                                    \
@@ -2977,8 +3005,11 @@ int analysis_impl(pdp_ctx* ctx, const int64_t* pid, const int64_t* pk, const dou
       PDP_KM(false, false, true) PDP_KM(true, false, true) PDP_KM(false, true, true) PDP_KM(true, true, true)
 #undef PDP_KM
     }
+    double* slots = (double*)(ws + L.slots);
     hipLaunchKernelGGL(km, dim3((unsigned)((waves + 3) / 4), cgroups), dim3(256), 0, stream, ppk, pref, pcnt, psum,
-                       npart, M, cfg_d, nconf, mflags, P, out->metrics, mom);
+                       npart, M, cfg_d, nconf, mflags, P, out->metrics, mom, slots, chunk);
+    hipLaunchKernelGGL(k_ana_fix, dim3((unsigned)((waves + 3) / 4), cgroups), dim3(256), 0, stream, ppk, M, nconf, nb,
+                       P, (const double*)slots, out->metrics, mom, chunk);
   }
   if (priv) {
     ProfScope ps_sel(ctx, PDP_STAGE_ANALYSIS_SELECT, stream);

@@ -147,3 +147,42 @@ def test_gpu_aggregate_errors_match_oracle(ex, private, laplace):
         np.testing.assert_allclose(sel.cpu().numpy(), sel2.numpy(), rtol=1e-12, atol=1e-9)
     again, _ = ex.aggregate_errors(metrics, prob, pids, mask, std, kinds, q, private)
     assert torch.equal(err, again)  # fixed-order reduction
+
+
+@pytest.mark.parametrize("C,private", [(64, True), (70, False)])
+def test_gpu_analysis_bitwise_deterministic(ex, C, private):
+    """Per-partition utility metrics are identical bit for bit run to run
+    (the reference merges accumulators in a fixed order, analysis/combiners.py:
+    228-310): partitions cut by a chunk boundary are merged from per-chunk
+    slots in chunk order (k_ana_fix), not with fp64 atomics.  Zipf(1.2) keys
+    over 3e6 rows: head partitions span hundreds of 2048-pair chunks.  Also
+    checked against the oracle (1e-9 relative)."""
+    import torch
+    from pipelinedp_amd import native
+    rng = np.random.default_rng(5 + C)
+    n, U, P = 3_000_000, 60_000, 2_000
+    pid, pk, val = o.synth_rows(n, U, P, seed=77 + C, zipf_s=1.2, value_lo=-3, value_hi=9)
+    cfgs = _cfgs(rng, C, private)
+    mask = native.METRIC_SUM | native.METRIC_COUNT | native.METRIC_PRIVACY_ID_COUNT
+    d = lambda a: torch.from_numpy(a).cuda()  # noqa: E731
+    runs = []
+    for _ in range(3):
+        m, prob, pids = ex.analyze(d(pid), d(pk), d(val), U, P, mask, cfgs)
+        torch.cuda.synchronize()
+        runs.append((m.cpu().numpy(), None if prob is None else prob.cpu().numpy()))
+    for m, prob in runs[1:]:
+        np.testing.assert_array_equal(m, runs[0][0])
+        if private:
+            np.testing.assert_array_equal(prob, runs[0][1])
+    sel = {native.SELECTION_NONE: None, native.SELECTION_TRUNCATED_GEOMETRIC: "truncated_geometric",
+           native.SELECTION_LAPLACE: "laplace", native.SELECTION_GAUSSIAN: "gaussian"}
+    ocfgs = [ao.AnalysisConfig(c.max_partitions_contributed, c.max_contributions_per_partition, c.min_sum_per_partition,
+                               c.max_sum_per_partition, sel[c.selection], c.selection_eps, c.selection_delta)
+             for c in cfgs[:4]]
+    ref = ao.per_partition(*ao.preaggregate(pid, pk, val), P, ocfgs, ["sum", "count", "privacy_id_count"],
+                           public=not private)
+    for c in range(4):
+        for b, name in enumerate(("sum", "count", "privacy_id_count")):
+            want = ref[name][c]
+            np.testing.assert_allclose(runs[0][0][c, b], want, rtol=1e-9, atol=1e-9 * (np.abs(want).max() + 1.0),
+                                       err_msg=f"{c} {name}")
