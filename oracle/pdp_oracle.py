@@ -863,6 +863,10 @@ def release(acc: Accumulators, bp: BoundParams, spec: ReleaseSpec, seed=0,
         eps, delta = spec.budgets["privacy_id_count"]
         out["privacy_id_count"] = _noisy(acc.row_count, seed, idx, STREAM_PID_COUNT, kind,
                                                          noise_scale(kind, eps, delta, L0, Linf), noise)
+    # a partition that private selection drops is not in the reference's result
+    # (dp_engine.py:312-362): its metrics are NaN (k_release computes no noise for it)
+    if spec.selection is not None:
+        out = {k: np.where(keep, v, np.nan) for k, v in out.items()}
     return keep, out
 
 

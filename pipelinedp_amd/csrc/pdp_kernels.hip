@@ -1281,6 +1281,10 @@ __global__ void k_release(const unsigned long long* __restrict__ row_count,
       }
     }
     keep[i] = kp;
+    if (!kp) {  // dropped by private selection: not in the result (dp_engine.py:312-362), no noise drawn
+      for (int k = 0; k < rp.nfields; ++k) out[(int64_t)k * P + i] = __longlong_as_double(0x7FF8000000000000ll);
+      continue;
+    }
     double f[5] = {0, 0, 0, 0, 0};  // variance, mean, count, sum, pid_count
     const int m = rp.metrics;
     if (m & (PDP_METRIC_VARIANCE | PDP_METRIC_MEAN)) {

@@ -121,9 +121,11 @@ def test_c3_release_selection_and_noise_full_size(ex):
     assert fields == ["mean", "count", "sum"]
     cnt = acc.count.to(torch.float64)
     mean = acc.x / torch.clamp(cnt, min=1.0) + (a + (b - a) / 2)
-    assert torch.equal(out0[1], cnt)
-    assert bool(((out0[0] - mean).abs() <= 1e-12 * mean.abs().clamp(min=1.0)).all())
-    assert torch.equal(keep0.bool(), acc.row_count > 0)  # noise-free: keep iff p(n) > 0
+    kept0 = keep0.bool()
+    assert torch.equal(kept0, acc.row_count > 0)  # noise-free: keep iff p(n) > 0
+    assert torch.equal(out0[1][kept0], cnt[kept0])
+    assert bool(((out0[0] - mean).abs() <= 1e-12 * mean.abs().clamp(min=1.0))[kept0].all())
+    assert bool(torch.isnan(out0[:, ~kept0]).all())  # dropped partitions: not in the result
 
     on = ReleaseConfig(mask, native.NOISE_LAPLACE, native.SELECTION_TRUNCATED_GEOMETRIC, eps, delta, 1,
                        add_noise=True, noise_seed=4)
@@ -135,10 +137,11 @@ def test_c3_release_selection_and_noise_full_size(ex):
     expect, var = float(p.sum()), float((p * (1 - p)).sum())
     kept = int(keep.sum())
     assert abs(kept - expect) <= 5 * math.sqrt(var) + 1, (kept, expect, var)
-    # Laplace(b = L0 * Linf / eps_count) on the released counts, b = 4 * 2 / 0.25
-    resid = (out[1] - cnt).cpu().numpy()
+    # Laplace(b = L0 * Linf / eps_count) on the released counts of the kept partitions, b = 4 * 2 / 0.25
+    kb = keep.bool()
+    resid = (out[1][kb] - cnt[kb]).cpu().numpy()
     bscale = L0 * Linf / 0.25
-    assert abs(np.mean(np.abs(resid)) - bscale) <= 5 * bscale / math.sqrt(P)
+    assert abs(np.mean(np.abs(resid)) - bscale) <= 5 * bscale / math.sqrt(len(resid))
 
 
 def test_c3_variance_full_size(ex):
@@ -199,7 +202,10 @@ def test_c3_variance_full_size(ex):
     keep, out, fields = ex.release(acc, off, cfg)
     torch.cuda.synchronize()
     assert sorted(fields) == ["count", "mean", "sum", "variance"]
-    f = {name: out[i] for i, name in enumerate(fields)}
+    kb = keep.bool()
+    assert torch.equal(kb, rc > 0)  # noise-free: keep iff p(n) > 0
+    f = {name: out[i][kb] for i, name in enumerate(fields)}
+    cf, x, y = cf[kb], x[kb], y[kb]
     den = cf.clamp(min=1.0)
     nmean = x / den
     var = y / den - nmean * nmean
@@ -209,7 +215,6 @@ def test_c3_variance_full_size(ex):
     assert bool(((f["mean"] - mean).abs() <= tol(mean)).all())
     assert bool(((f["variance"] - var).abs() <= tol(var) + 1e-12 * half * half).all())
     assert bool(((f["sum"] - mean * cf).abs() <= tol(mean * cf)).all())
-    assert torch.equal(keep.bool(), rc > 0)  # noise-free: keep iff p(n) > 0
 
 
 def test_c4_shard_binding_invariants(ex):
