@@ -2789,7 +2789,7 @@ int keep_table(int selection, double eps, double delta, int64_t k, std::vector<d
 
 struct AnaLayout {
   size_t recs_a, recs_b, flags, ppk, pref, pcnt, psum, npart, pbeg, mom, cfg, keep, hist, off, counters, status, slots,
-      total;
+      slots2, total;
   AnaGroups groups{};  // distinct L0 values (G = 0: more than kAnaMaxGroups)
   int64_t tiles;
   std::vector<AnaCfg> cfgs;  // keep pointers are offsets until bound to the workspace
@@ -2857,7 +2857,9 @@ int ana_layout(int64_t n, int64_t U, int64_t P, const pdp_analysis_config* cfgs,
   L.status = take((size_t)L.tiles * kStatusStride * 8);
   // k_ana_metrics' chunk-boundary partials: [chunk][head, tail][kAnaSlotFields][configurations / 64 * 64]
   const size_t chunk = (size_t)kAnaChunk * (size_t)((nconf + 63) / 64);
-  L.slots = take((n1 + chunk - 1) / chunk * 2 * kAnaSlotFields * (size_t)((nconf + 63) / 64 * 64) * 8);
+  const size_t nchunks = (n1 + chunk - 1) / chunk;
+  L.slots = take(nchunks * 2 * kAnaSlotFields * (size_t)((nconf + 63) / 64 * 64) * 8);
+  L.slots2 = take((nchunks + kAnaFixGroup - 1) / kAnaFixGroup * 2 * kAnaSlotFields * (size_t)((nconf + 63) / 64 * 64) * 8);
   L.total = o;
   return 0;
 }
@@ -3012,8 +3014,18 @@ int analysis_impl(pdp_ctx* ctx, const int64_t* pid, const int64_t* pk, const dou
     double* slots = (double*)(ws + L.slots);
     hipLaunchKernelGGL(km, dim3((unsigned)((waves + 3) / 4), cgroups), dim3(256), 0, stream, ppk, pref, pcnt, psum,
                        npart, M, cfg_d, nconf, mflags, P, out->metrics, mom, slots, chunk, (int)!priv);
-    hipLaunchKernelGGL(k_ana_fix, dim3((unsigned)((waves + 3) / 4), cgroups), dim3(256), 0, stream, ppk, M, nconf, nb,
-                       P, (const double*)slots, out->metrics, mom, chunk);
+    // fixed-order merge of the chunk-boundary partials, by levels of kAnaFixGroup units
+    double* lvl[2] = {slots, (double*)(ws + L.slots2)};
+    int64_t nunits = waves, ulen = chunk;
+    for (int level = 0;; ++level) {
+      const int G = nunits > kAnaFixGroup ? kAnaFixGroup : 0;
+      hipLaunchKernelGGL(k_ana_fix, dim3((unsigned)((nunits + 3) / 4), cgroups), dim3(256), 0, stream, ppk, M, ulen,
+                         nunits, G, nconf, nb, P, (const double*)lvl[level & 1], lvl[(level + 1) & 1], out->metrics,
+                         mom);
+      if (G == 0) break;
+      nunits = (nunits + G - 1) / G;
+      ulen *= G;
+    }
   }
   if (priv) {
     ProfScope ps_sel(ctx, PDP_STAGE_ANALYSIS_SELECT, stream);
