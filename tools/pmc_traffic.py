@@ -108,7 +108,7 @@ def main():
     src, rnd = sys.argv[1], sys.argv[2]
     prof = os.path.join(ROOT, "profiles")
     os.makedirs(prof, exist_ok=True)
-    for w in ("c3", "c4", "c2", "c5"):
+    for w in ("c3", "c4", "c2", "c5", "c3v"):
         kt = os.path.join(src, f"kt_{w}", "run_kernel_stats.csv")
         if os.path.exists(kt):
             shutil.copy(kt, os.path.join(prof, f"{rnd}_kernel_stats_{w}.csv"))

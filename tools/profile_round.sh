@@ -35,7 +35,7 @@ for w in ${PROFILE_WORKLOADS:-c3 c4}; do
   run "sq_$w" 240 rocprofv3 --pmc $SQ -T -f csv -d "$O/sq_$w" -o run -- \
     python -u bench.py --workload $w --steps 1 --warmup 1 --no-cpu-baseline --no-profile "$@"
 done
-for w in ${BENCH_WORKLOADS:-c2 c5}; do
+for w in ${BENCH_WORKLOADS:-c2 c5 c3v}; do
   run "bench_$w" 300 python -u bench.py --workload $w --no-cpu-baseline "$@"
   tail -1 "$O/bench_$w.out" | cut -c1-300
   run "kt_$w" 300 rocprofv3 --kernel-trace --stats -T -f csv -d "$O/kt_$w" -o run -- \
