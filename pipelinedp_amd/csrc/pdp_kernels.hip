@@ -120,6 +120,29 @@ __device__ __forceinline__ void st_rec(Rec* p, const Rec& r) {
 
 constexpr uint32_t kK4EmptyKey = 0xFFFFFFFFu;  // K4 empty pair slot (pdp_reduce.inc kK4Empty)
 
+// K4 12-byte pair records (pdp_reduce.inc): {key, x lo, x hi} with key = pk << cb | (count - 1) (the y
+// records' count is 0 -> key = pk << cb); an empty slot keeps key 0xFFFFFFFF.  In registers and LDS a
+// record stays a Rec (pid slot = key, pk slot unused).
+__device__ __forceinline__ Rec k4_pack12(Rec r, int cb) {
+  if (r.pid != kK4EmptyKey) r.pid = (r.pid << cb) | (r.pk > 0u ? r.pk - 1u : 0u);
+  return r;
+}
+__device__ __forceinline__ Rec k4_ld12(const Rec* base, int64_t i) {
+  const uint32_t* p = reinterpret_cast<const uint32_t*>(base) + 3 * i;
+  Rec r;
+  r.pid = p[0];
+  r.pk = 0u;
+  r.val = __longlong_as_double((long long)(((uint64_t)p[2] << 32) | p[1]));
+  return r;
+}
+__device__ __forceinline__ void k4_st12(Rec* base, int64_t i, const Rec& r) {
+  uint32_t* p = reinterpret_cast<uint32_t*>(base) + 3 * i;
+  const uint64_t b = (uint64_t)__double_as_longlong(r.val);
+  p[0] = r.pid;
+  p[1] = (uint32_t)b;
+  p[2] = (uint32_t)(b >> 32);
+}
+
 struct KeySpec {
   int mode;  // 0: key = pid >> low ; 1: key = (pid << pkb) | pk ; 3: key = (pid, bits(val)) 96-bit ;
              // 4: bucketed pid: passes with shift >= 64 take the bucket digit (pid * mult) >> 32, others pid bits ;
@@ -137,6 +160,7 @@ struct KeySpec {
   int ablate;  // kDebugNoLookback / kDebugLinearWrite (timing ablations, results invalid)
   int xcd_remap;  // reduce-then-scan passes: blocks sharing an XCD take one contiguous run of tiles
   int64_t cap;  // mode 6: records the output holds; a scatter position beyond it is reported, not written
+  int p12cb;    // K4 12-byte pair records: count bits below the partition id in the key (pdp_reduce.inc)
 };
 
 // How a row's value feeds the accumulators (combiners.py:254-261, 305-311,
@@ -588,7 +612,9 @@ __device__ __forceinline__ uint32_t xcd_tile(uint32_t b, uint32_t nwg) {
   return (x < r ? x * (q + 1u) : r * (q + 1u) + (x - r) * q) + b / 8u;
 }
 
-template <bool SOA, bool TAG = false>
+// P12 (K4 pair passes with 12-byte records, pdp_reduce.inc): 1 = 16-B pair slots {pk, count, x} in,
+// 12-B records {key = pk << cb | count - 1, x} out; 2 = 12-B records in and out.
+template <bool SOA, bool TAG = false, int P12 = 0>
 __device__ __forceinline__ void onesweep_body(
     const int64_t* __restrict__ pid, const int64_t* __restrict__ pk, const double* __restrict__ val,
     const Rec* __restrict__ rin, Rec* __restrict__ rout, int64_t n_in,
@@ -695,7 +721,12 @@ __device__ __forceinline__ void onesweep_body(
     for (int k = g; k < g + kRecGroup && k < kItems; ++k) {
       const int64_t idx = base + k * 64;
       const int64_t ic = full ? idx : (idx < last ? idx : last);
-      r[k] = ld_rec(ic < split ? rin + ic : rin2 + (ic - split));
+      if constexpr (P12 == 2) {
+        r[k] = k4_ld12(rin, ic);
+      } else {
+        r[k] = ld_rec(ic < split ? rin + ic : rin2 + (ic - split));
+        if constexpr (P12 == 1) r[k] = k4_pack12(r[k], ks.p12cb);
+      }
     }
 #pragma unroll
     for (int k = g; k < g + kRecGroup && k < kItems; ++k) {
@@ -885,7 +916,8 @@ __device__ __forceinline__ void onesweep_body(
           atomicOr(&counters[kCtrErr], 4ull);
           continue;
         }
-        st_rec(rout + q, rc);
+        if constexpr (P12 != 0) k4_st12(rout, q, rc);
+        else st_rec(rout + q, rc);
         if constexpr (TAG) tag_out[q] = rc.pid;
       }
     }
@@ -930,6 +962,13 @@ __global__ __launch_bounds__(kThreads, PDP_OS_OCC) void k_bucket_pass(PDP_ONESWE
 // K4 pair records by partition block (pdp_reduce.inc)
 __global__ __launch_bounds__(kThreads, PDP_OS_OCC) void k_pair_pass(PDP_ONESWEEP_ARGS) {
   onesweep_body<false, false>(PDP_ONESWEEP_PASS);
+}
+// ... with 12-byte pair records: the first pass (16-B slots in), later passes (12-B in)
+__global__ __launch_bounds__(kThreads, PDP_OS_OCC) void k_pair_pass12_first(PDP_ONESWEEP_ARGS) {
+  onesweep_body<false, false, 1>(PDP_ONESWEEP_PASS);
+}
+__global__ __launch_bounds__(kThreads, PDP_OS_OCC) void k_pair_pass12(PDP_ONESWEEP_ARGS) {
+  onesweep_body<false, false, 2>(PDP_ONESWEEP_PASS);
 }
 
 // ---------------------------------------------------------------------------
@@ -2220,6 +2259,8 @@ struct K4Plan {
   int passes;
   int shift[kK4MaxPasses], bits[kK4MaxPasses];
   int fx, fy;  // fixed-point exponents: q = rint(x * 2^f)
+  int cb;      // count bits of a 12-byte pair record's key
+  bool p12;    // pair passes move 12-byte records {pk << cb | count - 1, x} (pk and count fit 31 bits)
 };
 
 // F = 62 - ceil(log2 M): |q| <= 2^62 for |x| <= M; sums of < 2^32 records stay exact in (lo, hi).
@@ -2260,6 +2301,10 @@ K4Plan k4_plan(const pdp_bound_params* bp, const SegParams& sp, int64_t n, int64
   else if (sp.xmode == kXRawSum) mx = std::max(std::fabs(sp.smin), std::fabs(sp.smax));
   k.fx = k4_exponent(mx);
   k.fy = k4_exponent(linf * half * half);
+  // a pair's count is at most L_inf (1 when the bounds are already enforced): 12-byte pair records when
+  // the partition id and count - 1 fit 31 bits (c4: 26 + 2) -- a quarter fewer pair-pass bytes than 16
+  k.cb = pdp::ceil_log2_u64((uint64_t)std::max(1.0, linf));
+  k.p12 = pkb + k.cb <= 31 && env_int("PDP_K4_P12", 1) != 0;
   return k;
 }
 
@@ -2274,6 +2319,7 @@ K4Red k4_red(const K4Plan& k, const SegParams& sp, int64_t P, bool y) {
   r.inv_hi = std::ldexp(1.0, 32 - f);
   r.inv_lo = std::ldexp(1.0, -f);
   r.chunk = std::max(4096, env_int("PDP_K4_CHUNK", (int)kK4Chunk));
+  r.cb = k.p12 ? k.cb : 0;
   return r;
 }
 
@@ -2291,7 +2337,8 @@ int k4_run(pdp_ctx* ctx, hipStream_t stream, const K4Plan& k, const K4Red& kr, b
   ks.xcd_remap = env_int("PDP_XCD_REMAP", 1);
   ks.mode = 6;
   ks.cap = std::min<int64_t>(total, buf_cap);  // the pairs (< total) land in buf1 / buf2
-  ks.low = kr.sh;
+  ks.low = kr.sh + (k.p12 ? k.cb : 0);  // 12-byte records: the block digit sits above the count bits
+  ks.p12cb = k.p12 ? k.cb : 0;
   ks.passes = k.passes;
   for (int i = 0; i < k.passes; ++i) {
     ks.shift[i] = k.shift[i];
@@ -2309,7 +2356,8 @@ int k4_run(pdp_ctx* ctx, hipStream_t stream, const K4Plan& k, const K4Red& kr, b
         ctx->tile_slot = kCtrTile0;
       }
       if (int rc = next_epoch(ctx, stream, status, status_bytes, ws)) return rc;
-      hipLaunchKernelGGL(k_pair_pass, dim3((unsigned)tiles), dim3(kThreads), 0, stream, (const int64_t*)nullptr,
+      auto pass_kern = !k.p12 ? k_pair_pass : p == 0 ? k_pair_pass12_first : k_pair_pass12;
+      hipLaunchKernelGGL(pass_kern, dim3((unsigned)tiles), dim3(kThreads), 0, stream, (const int64_t*)nullptr,
                          (const int64_t*)nullptr, (const double*)nullptr, src, dst, (int64_t)0, counters,
                          p == 0 ? (int)kCtrK4In : (int)kCtrK4Pairs, ks, p, off + p * kHist, status, ctx->epoch,
                          counters, (int)ctx->tile_slot++, (const unsigned int*)nullptr, (uint32_t*)nullptr,
@@ -2324,19 +2372,22 @@ int k4_run(pdp_ctx* ctx, hipStream_t stream, const K4Plan& k, const K4Red& kr, b
   const int64_t chunks = (total + kr.chunk - 1) / kr.chunk;
   const bool scratch = (y || kr.want_x) && chunks > 1;
   if (scratch)
-    hipLaunchKernelGGL(k4_zero_shared, dim3((unsigned)(chunks - 1)), dim3(kThreads), 0, stream, src, counters, kr.sh,
-                       kr.P, kr.chunk, s_lo, s_hi, s_fl);
-  auto kern = y ? (kr.sh == kK4ShMax ? k4_reduce<true, kK4ShMax> : k4_reduce<true, kK4ShMax - 1>)
-               : (kr.sh == kK4ShMax ? k4_reduce<false, kK4ShMax> : k4_reduce<false, kK4ShMax - 1>);
+    hipLaunchKernelGGL(k.p12 ? k4_zero_shared<1> : k4_zero_shared<0>, dim3((unsigned)(chunks - 1)), dim3(kThreads), 0,
+                       stream, src, counters, kr.sh, kr.P, kr.chunk, s_lo, s_hi, s_fl, kr.cb);
+  decltype(&k4_reduce<true, kK4ShMax, 0>) kern;
+  if (k.p12)
+    kern = y ? (kr.sh == kK4ShMax ? k4_reduce<true, kK4ShMax, 1> : k4_reduce<true, kK4ShMax - 1, 1>)
+             : (kr.sh == kK4ShMax ? k4_reduce<false, kK4ShMax, 1> : k4_reduce<false, kK4ShMax - 1, 1>);
+  else
+    kern = y ? (kr.sh == kK4ShMax ? k4_reduce<true, kK4ShMax, 0> : k4_reduce<true, kK4ShMax - 1, 0>)
+             : (kr.sh == kK4ShMax ? k4_reduce<false, kK4ShMax, 0> : k4_reduce<false, kK4ShMax - 1, 0>);
   hipLaunchKernelGGL(kern, dim3((unsigned)chunks), dim3(kK4Threads), 0, stream, src, counters, kr, acc, s_lo, s_hi,
                      s_fl);
   if (scratch) {
-    if (y)
-      hipLaunchKernelGGL(k4_finalize<true>, dim3((unsigned)(chunks - 1)), dim3(kThreads), 0, stream, src, counters,
-                         kr, acc, s_lo, s_hi, s_fl);
-    else
-      hipLaunchKernelGGL(k4_finalize<false>, dim3((unsigned)(chunks - 1)), dim3(kThreads), 0, stream, src, counters,
-                         kr, acc, s_lo, s_hi, s_fl);
+    auto fin = y ? (k.p12 ? k4_finalize<true, 1> : k4_finalize<true, 0>)
+                 : (k.p12 ? k4_finalize<false, 1> : k4_finalize<false, 0>);
+    hipLaunchKernelGGL(fin, dim3((unsigned)(chunks - 1)), dim3(kThreads), 0, stream, src, counters, kr, acc, s_lo,
+                       s_hi, s_fl);
   }
   HIP_TRY(hipGetLastError());
   return 0;

@@ -587,3 +587,25 @@ def test_heavy_single_group_generic_path(ex):
         ref = o.bound_and_accumulate(pid, pk, val, P, bp, "hash", seed=5)
         check_acc(ref, rc, cnt, x, y, mask, val)
         assert dt < 0.5, dt
+
+
+@pytest.mark.parametrize("cfgi", [0, 2, 9, 11, 19, 21])
+def test_k4_pair_record_forms_bitwise_equal(ex, cfgi, monkeypatch):
+    """K4's pair passes move 12-byte records {pk << cb | count - 1, x} when the
+    partition id and count fit 31 bits, 16-byte {pk, count, x} otherwise
+    (PDP_K4_P12=0 forces them): the fixed-point sums are integers, so both
+    forms give identical accumulators, sums included."""
+    n, U, P, z, L0, Linf, vb, pb, mask = CONFIGS[cfgi]
+    pid, pk, val = o.synth_rows(n, U, P, seed=700 + cfgi, zipf_s=z, value_lo=-5, value_hi=15)
+    bp = o.BoundParams(L0, Linf, *(vb or (None, None)), *(pb or (None, None)))
+    need_val = bool(mask & (2 | 4 | 8))
+    runs = []
+    for p12 in ("1", "0"):
+        monkeypatch.setenv("PDP_K4_P12", p12)
+        _, _, rc, cnt, x, y = run_gpu(ex, pid, pk, val if need_val else None, U, P, bp, mask, seed=5 + cfgi)
+        runs.append((rc, cnt, x, y))
+    for a, b in zip(*runs):
+        if a is None:
+            assert b is None
+        else:
+            np.testing.assert_array_equal(a, b)
