@@ -23,7 +23,10 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <string>
+#include <tuple>
 #include <vector>
 
 #include "pdp_hip.h"
@@ -2838,6 +2841,26 @@ int keep_table(int selection, double eps, double delta, int64_t k, std::vector<d
   return 0;
 }
 
+// keep_table memoised per (selection, eps, delta, k): a configuration sweep
+// repeats each L0 for every L_inf, and the truncated-geometric tables cost
+// milliseconds of host time per call (bounded process-wide cache).
+int keep_table_cached(int selection, double eps, double delta, int64_t k, std::vector<double>& t) {
+  using Key = std::tuple<int, double, double, int64_t>;
+  static std::mutex mu;
+  static std::map<Key, std::vector<double>> cache;
+  const Key key{selection, eps, delta, k};
+  std::lock_guard<std::mutex> lock(mu);
+  auto it = cache.find(key);
+  if (it == cache.end()) {
+    std::vector<double> v;
+    if (int rc = keep_table(selection, eps, delta, k, v)) return rc;
+    if (cache.size() >= 1024) cache.clear();
+    it = cache.emplace(key, std::move(v)).first;
+  }
+  t = it->second;
+  return 0;
+}
+
 struct AnaLayout {
   size_t recs_a, recs_b, flags, ppk, pref, pcnt, psum, npart, pbeg, mom, cfg, keep, hist, off, counters, status, slots,
       slots2, total;
@@ -2869,6 +2892,7 @@ int ana_layout(int64_t n, int64_t U, int64_t P, const pdp_analysis_config* cfgs,
   L.cfg = take((size_t)nconf * sizeof(AnaCfg));
   L.cfgs.assign((size_t)nconf, AnaCfg{});
   L.keep_all.clear();
+  std::map<std::tuple<int, double, double, int64_t>, size_t> shared;  // identical tables share one copy
   std::vector<double> t;
   for (int c = 0; c < nconf; ++c) {
     const pdp_analysis_config& a = cfgs[c];
@@ -2876,15 +2900,21 @@ int ana_layout(int64_t n, int64_t U, int64_t P, const pdp_analysis_config* cfgs,
       return fail(PDP_ERR_INVALID_ARG, "all configurations must use private selection, or none (public partitions)");
     if (a.max_partitions_contributed < 1 || a.max_contributions_per_partition < 1)
       return fail(PDP_ERR_INVALID_ARG, "contribution bounds must be positive");
-    if (int rc = keep_table(a.selection, a.selection_eps, a.selection_delta, a.max_partitions_contributed, t)) return rc;
+    const auto key = std::make_tuple(a.selection, a.selection_eps, a.selection_delta, a.max_partitions_contributed);
+    auto sh = shared.find(key);
+    if (int rc = keep_table_cached(a.selection, a.selection_eps, a.selection_delta, a.max_partitions_contributed, t))
+      return rc;
+    if (sh == shared.end()) {
+      sh = shared.emplace(key, L.keep_all.size()).first;
+      L.keep_all.insert(L.keep_all.end(), t.begin(), t.end());
+    }
     AnaCfg& g = L.cfgs[c];
     g.l0 = (double)a.max_partitions_contributed;
     g.linf = (double)a.max_contributions_per_partition;
     g.smin = a.min_sum_per_partition;
     g.smax = a.max_sum_per_partition;
-    g.keep = (const double*)(uintptr_t)L.keep_all.size();  // offset, bound later
+    g.keep = (const double*)(uintptr_t)sh->second;  // offset, bound later
     g.keep_len = (int64_t)t.size();
-    L.keep_all.insert(L.keep_all.end(), t.begin(), t.end());
     g.grp = -1;
     for (int j = 0; j < L.groups.G; ++j)
       if (L.groups.l0[j] == g.l0) g.grp = j;
