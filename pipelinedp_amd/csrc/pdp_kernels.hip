@@ -1710,7 +1710,7 @@ struct pdp_ctx {
   std::vector<hipEvent_t> pool;
   double prof_ms[PDP_NUM_STAGES] = {};
   int64_t prof_n[PDP_NUM_STAGES] = {};
-  void* last_ws = nullptr;
+  void* status_at = nullptr;  // look-back status region cleared for the current epoch run (next_epoch)
   size_t status_ok = 0;  // bytes of the look-back status region cleared for the current epoch run
   uint32_t epoch = 0;
   pdp_stats stats{};
@@ -1789,10 +1789,18 @@ struct ProfScope {
 
 int env_int(const char* name, int def);
 
-int next_epoch(pdp_ctx* ctx, hipStream_t stream, unsigned long long* status, size_t status_bytes, void* ws) {
-  if (ctx->last_ws != ws || ctx->epoch >= 0xFFFE || status_bytes > ctx->status_ok) {
+// Look-back status words carry the epoch of their pass, so a region cleared
+// once serves 0xFFFE passes.  The region is cleared again when a pass needs
+// more of it, when it moves (another layout of the workspace: the bytes held
+// records or other scratch), and on the first pass of every API call
+// (ctx->status_at reset on entry: the caller owns the workspace between calls).
+// Round 4: the check was keyed on the workspace base, so a utility analysis
+// after a larger aggregate on the same workspace met stale record bytes that
+// read as published status words -> wrong digit bases -> out-of-range scatter.
+int next_epoch(pdp_ctx* ctx, hipStream_t stream, unsigned long long* status, size_t status_bytes) {
+  if (ctx->status_at != (void*)status || ctx->epoch >= 0xFFFE || status_bytes > ctx->status_ok) {
     HIP_TRY(hipMemsetAsync(status, 0, status_bytes, stream));
-    ctx->last_ws = ws;
+    ctx->status_at = status;
     ctx->status_ok = status_bytes;
     ctx->epoch = 0;
   }
@@ -1827,7 +1835,7 @@ struct TileScan {
 };
 
 TileScan tile_scan_bufs(pdp_ctx* ctx, unsigned long long* status, int64_t tiles) {
-  ctx->last_ws = nullptr;
+  ctx->status_at = nullptr;
   TileScan ts;
   ts.tile_cnt = (unsigned int*)status;
   ts.chunk = ts.tile_cnt + (size_t)tiles * 256;
@@ -1881,7 +1889,7 @@ int sort_recs(pdp_ctx* ctx, Rec* a, Rec* b, int64_t m, const KeySpec& ks, unsign
       tile_scan(ts, off + p * kHist, stream);
       bases = ts.tile_cnt;
     } else {
-      int rc = next_epoch(ctx, stream, status, status_bytes, ws);
+      int rc = next_epoch(ctx, stream, status, std::min(status_bytes, (size_t)tiles * kStatusStride * 8));
       if (rc) return rc;
     }
     hipLaunchKernelGGL(k_onesweep, dim3((unsigned)tiles), dim3(kThreads), 0, stream,
@@ -2358,7 +2366,7 @@ int k4_run(pdp_ctx* ctx, hipStream_t stream, const K4Plan& k, const K4Red& kr, b
         HIP_TRY(hipMemsetAsync(counters + kCtrTile0, 0, (kNumCounters - kCtrTile0) * 8, stream));
         ctx->tile_slot = kCtrTile0;
       }
-      if (int rc = next_epoch(ctx, stream, status, status_bytes, ws)) return rc;
+      if (int rc = next_epoch(ctx, stream, status, status_bytes)) return rc;
       auto pass_kern = !k.p12 ? k_pair_pass : p == 0 ? k_pair_pass12_first : k_pair_pass12;
       hipLaunchKernelGGL(pass_kern, dim3((unsigned)tiles), dim3(kThreads), 0, stream, (const int64_t*)nullptr,
                          (const int64_t*)nullptr, (const double*)nullptr, src, dst, (int64_t)0, counters,
@@ -2476,6 +2484,7 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
   const size_t status_bytes = (size_t)L.tiles * kStatusStride * 8;
   HIP_TRY(hipMemsetAsync(ws + L.hist, 0, L.status - L.hist, stream));  // hist, off, counters
   ctx->tile_slot = kCtrTile0;
+  ctx->status_at = nullptr;  // first look-back pass of this call clears its status words (next_epoch)
   // K4 (pdp_reduce.inc): pair records into `slots` (+ the y slots), then pair passes + reduction
   unsigned int* k4rep = (unsigned int*)(ws + L.k4rep);
   unsigned long long* k4lo = (unsigned long long*)(ws + L.k4s);
@@ -2604,7 +2613,7 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
       tile_scan(ts, off + p * kHist, stream);
       bases = ts.tile_cnt;
     } else {
-      int rc = next_epoch(ctx, stream, status, status_bytes, workspace);
+      int rc = next_epoch(ctx, stream, status, status_bytes);
       if (rc) return rc;
     }
     ProfScope ps(ctx, p == 0 ? PDP_STAGE_ONESWEEP_FIRST : PDP_STAGE_ONESWEEP_REST, stream);
@@ -3003,6 +3012,7 @@ int analysis_impl(pdp_ctx* ctx, const int64_t* pid, const int64_t* pk, const dou
   if (out->metrics) HIP_TRY(hipMemsetAsync(out->metrics, 0, (size_t)nconf * nb * 5 * P * 8, stream));
   if (mom) HIP_TRY(hipMemsetAsync(mom, 0, (size_t)nconf * 4 * P * 8, stream));
   ctx->tile_slot = kCtrTile0;
+  ctx->status_at = nullptr;  // first look-back pass of this call clears its status words (next_epoch)
   ctx->stats = pdp_stats{};
   const size_t status_bytes = (size_t)L.tiles * kStatusStride * 8;
   const int pkbits = std::max(1, pdp::ceil_log2_u64((uint64_t)P + 1));

@@ -186,3 +186,32 @@ def test_gpu_analysis_bitwise_deterministic(ex, C, private):
             want = ref[name][c]
             np.testing.assert_allclose(runs[0][0][c, b], want, rtol=1e-9, atol=1e-9 * (np.abs(want).max() + 1.0),
                                        err_msg=f"{c} {name}")
+
+
+def test_analysis_after_aggregate_on_one_workspace(ex):
+    """Workspace reuse across entry points: an aggregate (its look-back passes
+    leave record bytes where the analysis layout keeps its look-back status
+    words) and then a utility analysis on the same executor and workspace give
+    the analysis result of a fresh executor, bit for bit.  Round 4 found the
+    status region's clear keyed on the workspace base instead of the region's
+    address: at full size the analysis sort met stale bytes that read as
+    published status words and scattered out of range (next_epoch)."""
+    import torch
+    from pipelinedp_amd import native
+    from pipelinedp_amd.executor import BoundConfig, HipExecutor
+    n, U, P = 4_000_000, 400_000, 2_000_000
+    pid, pk, val = ex.generate(n, U, P, seed=91, zipf_s=0.0, lo=0.0, hi=10.0)
+    mask = native.METRIC_COUNT | native.METRIC_SUM
+    ex.accumulate(pid, pk, val, U, P, BoundConfig(mask, 32, 4, 0.0, 10.0, sampling_seed=3))
+    torch.cuda.synchronize()
+    rng = np.random.default_rng(12)
+    na, Ua, Pa = 1_000_000, 50_000, 70_000
+    apid, apk, aval = ex.generate(na, Ua, Pa, seed=92, zipf_s=1.1, lo=-3.0, hi=9.0)
+    cfgs = _cfgs(rng, 8, True)
+    amask = native.METRIC_SUM | native.METRIC_COUNT | native.METRIC_PRIVACY_ID_COUNT
+    m1, p1, _ = ex.analyze(apid, apk, aval, Ua, Pa, amask, cfgs)
+    fresh = HipExecutor(0)
+    m2, p2, _ = fresh.analyze(apid, apk, aval, Ua, Pa, amask, cfgs)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(m1.cpu().numpy(), m2.cpu().numpy())
+    np.testing.assert_array_equal(p1.cpu().numpy(), p2.cpu().numpy())
