@@ -127,7 +127,7 @@ constexpr uint32_t kK4EmptyKey = 0xFFFFFFFFu;  // K4 empty pair slot (pdp_reduce
 // records' count is 0 -> key = pk << cb); an empty slot keeps key 0xFFFFFFFF.  In registers and LDS a
 // record stays a Rec (pid slot = key, pk slot unused).
 __device__ __forceinline__ Rec k4_pack12(Rec r, int cb) {
-  if (r.pid != kK4EmptyKey) r.pid = (r.pid << cb) | (r.pk > 0u ? r.pk - 1u : 0u);
+  if (r.pid != kK4EmptyKey) r.pid = (r.pid << cb) | ((r.pk > 0u ? r.pk - 1u : 0u) & ((1u << cb) - 1u));
   return r;
 }
 __device__ __forceinline__ Rec k4_ld12(const Rec* base, int64_t i) {
@@ -2314,7 +2314,9 @@ K4Plan k4_plan(const pdp_bound_params* bp, const SegParams& sp, int64_t n, int64
   k.fy = k4_exponent(linf * half * half);
   // a pair's count is at most L_inf (1 when the bounds are already enforced): 12-byte pair records when
   // the partition id and count - 1 fit 31 bits (c4: 26 + 2) -- a quarter fewer pair-pass bytes than 16
-  k.cb = pdp::ceil_log2_u64((uint64_t)std::max(1.0, linf));
+  // the count is used only by COUNT / MEAN / VARIANCE; without it K2 does not sample rows (the slot's count
+  // is the group's row count, unbounded), so the key carries no count bits
+  k.cb = sp.want_count ? pdp::ceil_log2_u64((uint64_t)std::max(1.0, linf)) : 0;
   k.p12 = pkb + k.cb <= 31 && env_int("PDP_K4_P12", 1) != 0;
   return k;
 }
@@ -3122,8 +3124,7 @@ int analysis_impl(pdp_ctx* ctx, const int64_t* pid, const int64_t* pk, const dou
     ProfScope ps_sel(ctx, PDP_STAGE_ANALYSIS_SELECT, stream);
     const int64_t blocks = std::min<int64_t>((P + kAnaSelWaves - 1) / kAnaSelWaves, 16384);
     if (L.groups.G > 0 && !env_int("PDP_ANA_SEL_LDS", 0)) {
-      const size_t lds = (size_t)std::max(L.groups.G * 128, kAnaCdfMax) * 8;
-      hipLaunchKernelGGL(k_ana_select_grouped, dim3((unsigned)std::min<int64_t>(P, 65536), cgroups), dim3(64), lds,
+      hipLaunchKernelGGL(k_ana_select_grouped, dim3((unsigned)std::min<int64_t>(P, 65536), cgroups), dim3(64), 0,
                          stream, pref, npart, pbeg, P, cfg_d, nconf, L.groups, (const double*)mom, out->prob_keep);
     } else {  // round-3 form: one launch per regime, lanes = configurations
       hipLaunchKernelGGL(k_ana_select<true>, dim3((unsigned)blocks, cgroups), dim3(64 * kAnaSelWaves), 0, stream, pref,

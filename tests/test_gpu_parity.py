@@ -609,3 +609,20 @@ def test_k4_pair_record_forms_bitwise_equal(ex, cfgi, monkeypatch):
             assert b is None
         else:
             np.testing.assert_array_equal(a, b)
+
+
+@pytest.mark.parametrize("p12", ["1", "0"])
+@pytest.mark.parametrize("cfgi", [0, 5, 9, 11, 17, 19, 21])
+def test_row_counts_only_match_oracle(ex, cfgi, p12, monkeypatch):
+    """Selection only (no COUNT / SUM: select_partitions' accumulate): K2 does
+    not sample rows then, so a pair slot's count is the group's row count, not
+    bounded by L_inf; the 12-byte K4 key must not carry count bits (a round-4
+    build OR-ed them into the partition id).  Row counts bit-exact vs the
+    oracle in both record forms."""
+    n, U, P, z, L0, Linf, vb, pb, _ = CONFIGS[cfgi]
+    pid, pk, _ = o.synth_rows(n, U, P, seed=900 + cfgi, zipf_s=z, value_lo=0, value_hi=1)
+    monkeypatch.setenv("PDP_K4_P12", p12)
+    bp = o.BoundParams(L0, Linf)
+    _, _, rc, cnt, x, y = run_gpu(ex, pid, pk, None, U, P, bp, 0, seed=11 + cfgi)
+    ref = o.bound_and_accumulate(pid, pk, None, P, bp, "hash", seed=11 + cfgi)
+    np.testing.assert_array_equal(rc, ref.row_count)
