@@ -342,7 +342,20 @@ __device__ __forceinline__ T block_max(T v, T* s_tmp) {
 #endif
 constexpr int kHistUnroll = PDP_HIST_UNROLL;  // rows per thread with loads in flight together (K0, K1u)
 
-template <bool SOA>
+// Utility-analysis record of a row (k_ana_pack restated for the fused first pass):
+// {pk, pid, value} for a row in range, the all-ones key (sorts last) otherwise;
+// `invalid` counts the out-of-range rows that are errors (pk >= P, or a public
+// row's pid out of range).
+__device__ __forceinline__ Rec ana_rec(int64_t a, int64_t b, double v, const KeySpec& ks, unsigned int& invalid) {
+  const bool ok = b >= 0 && b < (int64_t)ks.num_parts && a >= 0 && a < (int64_t)ks.num_pids;
+  invalid += b >= (int64_t)ks.num_parts || (b >= 0 && (a < 0 || a >= (int64_t)ks.num_pids));
+  return ok ? Rec{(uint32_t)b, (uint32_t)a, v} : Rec{0xFFFFFFFFu, 0xFFFFFFFFu, 0.0};
+}
+
+// MODE 0: records; 1: SoA columns (rows out of range dropped); 2: SoA columns of the utility
+// analysis (the records k_ana_pack would write: {pk, pid}, rows out of range as the all-ones
+// key that sorts last, pdp_analysis.inc)
+template <int MODE>
 __global__ __launch_bounds__(kThreads) void k_histogram(const int64_t* __restrict__ pid,
                                                         const int64_t* __restrict__ pk,
                                                         const Rec* __restrict__ rin, int64_t n,
@@ -361,7 +374,7 @@ __global__ __launch_bounds__(kThreads) void k_histogram(const int64_t* __restric
 #pragma unroll
     for (int u = 0; u < kHistUnroll; ++u) {
       const int64_t i = i0 + (int64_t)u * kThreads, ic = i < n ? i : n - 1;
-      if (SOA) {
+      if (MODE != 0) {
         a[u] = pid[ic];
         b[u] = pk[ic];
       } else {
@@ -371,7 +384,9 @@ __global__ __launch_bounds__(kThreads) void k_histogram(const int64_t* __restric
 #pragma unroll
     for (int u = 0; u < kHistUnroll; ++u) {
       if (i0 + (int64_t)u * kThreads >= n) break;
-      if (SOA) {
+      if (MODE == 2) {
+        r[u] = ana_rec(a[u], b[u], 0.0, ks, invalid);
+      } else if (MODE == 1) {
         if (b[u] < 0 || b[u] >= (int64_t)ks.num_parts || a[u] < 0 || a[u] >= (int64_t)ks.num_pids) {
           if (b[u] >= 0) ++invalid;
           atomicAdd(&sh[256], 1u);
@@ -617,7 +632,9 @@ __device__ __forceinline__ uint32_t xcd_tile(uint32_t b, uint32_t nwg) {
 
 // P12 (K4 pair passes with 12-byte records, pdp_reduce.inc): 1 = 16-B pair slots {pk, count, x} in,
 // 12-B records {key = pk << cb | count - 1, x} out; 2 = 12-B records in and out.
-template <bool SOA, bool TAG = false, int P12 = 0>
+// ANA (with SOA): the utility analysis' first pass -- the columns become the {pk, pid, value} records of
+// ana_rec (k_ana_pack fused in); no row is dropped (out-of-range rows carry the all-ones key).
+template <bool SOA, bool TAG = false, int P12 = 0, bool ANA = false>
 __device__ __forceinline__ void onesweep_body(
     const int64_t* __restrict__ pid, const int64_t* __restrict__ pk, const double* __restrict__ val,
     const Rec* __restrict__ rin, Rec* __restrict__ rout, int64_t n_in,
@@ -694,7 +711,11 @@ __device__ __forceinline__ void onesweep_body(
       const bool valid = full || base + k * 64 <= last;
       r[k].pid = (uint32_t)a[k];
       r[k].pk = (uint32_t)b[k];
-      if constexpr (TAG) {
+      if constexpr (ANA) {
+        unsigned int inv = 0;  // counted by k_histogram<2>
+        r[k] = ana_rec(a[k], b[k], r[k].val, ks, inv);
+        d = digit_of(ks, pass, r[k]);
+      } else if constexpr (TAG) {
         // placed unless the privacy id is out of range (k_histogram_tiles<true>); a non-public row
         // (pk < 0) is tagged dropped, an out-of-range pk is an error
         if (a[k] < 0 || a[k] >= (int64_t)ks.num_pids) {
@@ -957,6 +978,10 @@ __global__ __launch_bounds__(kThreads, PDP_OS_OCC) void k_onesweep(PDP_ONESWEEP_
 // SoA columns -> records (first pass of the pid sort, non-public rows dropped)
 __global__ __launch_bounds__(kThreads, PDP_OS_OCC) void k_sort_first(PDP_ONESWEEP_ARGS) {
   onesweep_body<true, false>(PDP_ONESWEEP_PASS);
+}
+// the utility analysis' first (pk, pid) pass from the SoA columns (pdp_analysis.inc)
+__global__ __launch_bounds__(kThreads, PDP_OS_OCC) void k_ana_sort_first(PDP_ONESWEEP_ARGS) {
+  onesweep_body<true, false, 0, true>(PDP_ONESWEEP_PASS);
 }
 // the L0 pre-filter's bucket pass (SoA columns -> tagged records + tags, pdp_filter.inc)
 __global__ __launch_bounds__(kThreads, PDP_OS_OCC) void k_bucket_pass(PDP_ONESWEEP_ARGS) {
@@ -1858,7 +1883,10 @@ void tile_scan(const TileScan& ts, const unsigned long long* off_pass, hipStream
 // sorted array pointer is returned in *out.
 int sort_recs(pdp_ctx* ctx, Rec* a, Rec* b, int64_t m, const KeySpec& ks, unsigned long long* hist,
               unsigned long long* off, unsigned long long* counters, unsigned long long* status, size_t status_bytes,
-              void* ws, hipStream_t stream, Rec** out, int stage = PDP_STAGE_GENERIC) {
+              void* ws, hipStream_t stream, Rec** out, int stage = PDP_STAGE_GENERIC,
+              const int64_t* soa_pid = nullptr, const int64_t* soa_pk = nullptr, const double* soa_val = nullptr) {
+  // soa_pk != null: the utility analysis' rows, packed by the histogram and the first pass themselves
+  // (k_histogram<2>, k_ana_sort_first); `a` is not read
   if (m <= 0 || ks.passes == 0) {
     *out = a;
     return 0;
@@ -1870,8 +1898,12 @@ int sort_recs(pdp_ctx* ctx, Rec* a, Rec* b, int64_t m, const KeySpec& ks, unsign
   }
   HIP_TRY(hipMemsetAsync(hist, 0, kMaxPasses * kHist * 8, stream));
   ProfScope prof_generic(ctx, stage, stream);
-  hipLaunchKernelGGL(k_histogram<false>, dim3(grid_for(m, kThreads, 2048)), dim3(kThreads), 0, stream,
-                     (const int64_t*)nullptr, (const int64_t*)nullptr, a, m, ks, hist, counters);
+  if (soa_pk)
+    hipLaunchKernelGGL(k_histogram<2>, dim3(grid_for(m, kThreads, 2048)), dim3(kThreads), 0, stream, soa_pid, soa_pk,
+                       (const Rec*)nullptr, m, ks, hist, counters);
+  else
+    hipLaunchKernelGGL(k_histogram<0>, dim3(grid_for(m, kThreads, 2048)), dim3(kThreads), 0, stream,
+                       (const int64_t*)nullptr, (const int64_t*)nullptr, a, m, ks, hist, counters);
   hipLaunchKernelGGL(k_offsets, dim3(1), dim3(kThreads), 0, stream, hist, off, ks.passes, m, counters,
                      (int)kCtrNGeneric);
   Rec* src = a;
@@ -1892,8 +1924,10 @@ int sort_recs(pdp_ctx* ctx, Rec* a, Rec* b, int64_t m, const KeySpec& ks, unsign
       int rc = next_epoch(ctx, stream, status, std::min(status_bytes, (size_t)tiles * kStatusStride * 8));
       if (rc) return rc;
     }
-    hipLaunchKernelGGL(k_onesweep, dim3((unsigned)tiles), dim3(kThreads), 0, stream,
-                       (const int64_t*)nullptr, (const int64_t*)nullptr, (const double*)nullptr, src, dst, m,
+    const bool soa = soa_pk && p == 0;
+    hipLaunchKernelGGL(soa ? k_ana_sort_first : k_onesweep, dim3((unsigned)tiles), dim3(kThreads), 0, stream,
+                       soa ? soa_pid : (const int64_t*)nullptr, soa ? soa_pk : (const int64_t*)nullptr,
+                       soa ? soa_val : (const double*)nullptr, soa ? (const Rec*)nullptr : src, dst, m,
                        counters, (int)kCtrNGeneric, ks, p, off + p * kHist, status, ctx->epoch, counters,
                        (int)ctx->tile_slot++, bases, (uint32_t*)nullptr, (const uint32_t*)nullptr,
                        (const Rec*)nullptr, (int64_t)INT64_MAX);
@@ -2594,7 +2628,7 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
       hipLaunchKernelGGL(fpl.on ? k_histogram_tiles<true> : k_histogram_tiles<false>, dim3(grid_for(L.tiles, 1, 4096)),
                          dim3(kThreads), 0, stream, cols->pid, cols->pk, n, ks, hist, ts.tile_cnt, counters);
     else
-      hipLaunchKernelGGL(k_histogram<true>, dim3(grid_for(n, kThreads, 2048)), dim3(kThreads), 0, stream,
+      hipLaunchKernelGGL(k_histogram<1>, dim3(grid_for(n, kThreads, 2048)), dim3(kThreads), 0, stream,
                          cols->pid, cols->pk, (const Rec*)nullptr, n, ks, hist, counters);
   }
   hipLaunchKernelGGL(k_offsets, dim3(1), dim3(kThreads), 0, stream, hist, off, ks.passes, n, counters,
@@ -3025,12 +3059,17 @@ int analysis_impl(pdp_ctx* ctx, const int64_t* pid, const int64_t* pk, const dou
     Rec* sorted = nullptr;
     if (pid) {
       // rows -> (pk, pid)-sorted records -> pairs
-      hipLaunchKernelGGL(k_ana_pack, dim3(g), dim3(kThreads), 0, stream, pid, pk, val, n, U, P, ra, counters);
       const int pidbits = std::max(1, pdp::ceil_log2_u64((uint64_t)U + 1));
       KeySpec ks = composite_spec(1, pkbits, pidbits, pidbits, (uint32_t)std::min<int64_t>(U, 0xFFFFFFFFll),
                                   (uint32_t)P);
+      // round 4: the packing is fused into the histogram and the first pass (c5: -0.94 ms of k_ana_pack,
+      // +8 B per row in the first pass); PDP_ANA_PACK=1 restores the separate pack
+      const bool fused = ks.passes > 0 && !env_int("PDP_ANA_PACK", 0);
+      if (!fused)
+        hipLaunchKernelGGL(k_ana_pack, dim3(g), dim3(kThreads), 0, stream, pid, pk, val, n, U, P, ra, counters);
       if (int rc = sort_recs(ctx, ra, rb, n, ks, hist, off, counters, status, status_bytes, workspace, stream, &sorted,
-                             PDP_STAGE_ANALYSIS_SORT))
+                             PDP_STAGE_ANALYSIS_SORT, fused ? pid : nullptr, fused ? pk : nullptr,
+                             fused ? val : nullptr))
         return rc;
       if (env_int("PDP_ANA_FLAGS", 0)) {  // round-3 form: per-row flags, scan, one thread per group start
         hipLaunchKernelGGL(k_ana_group_flags, dim3(g), dim3(kThreads), 0, stream, sorted, n, flags);
