@@ -506,6 +506,51 @@ __global__ __launch_bounds__(kThreads) void k_tile_counts(const Rec* __restrict_
   }
 }
 
+// The same for the K4 pair passes (reduce-then-scan instead of decoupled
+// look-back; round 4): records read as the pass reads them (P12 1: 16-B slots
+// packed to 12-byte keys, 2: 12-byte records; pass 0 also reads the generic
+// path's pairs after `split`), empty slots not counted.
+template <int P12>
+__global__ __launch_bounds__(kThreads) void k_pair_tile_counts(const Rec* __restrict__ rin,
+                                                               const Rec* __restrict__ rin2, int64_t split,
+                                                               const unsigned long long* __restrict__ counters_n,
+                                                               int n_slot, KeySpec ks, int pass, int64_t tiles,
+                                                               unsigned int* __restrict__ tile_cnt) {
+  __shared__ unsigned int st[256];
+  const int t = threadIdx.x;
+  st[t] = 0;
+  __syncthreads();
+  const int64_t n = (int64_t)counters_n[n_slot];
+  for (int64_t tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
+    const int64_t base = tile * kTile + t;
+#pragma unroll
+    for (int g = 0; g < kItems; g += kHistUnroll) {
+      Rec r[kHistUnroll];
+#pragma unroll
+      for (int u = 0; u < kHistUnroll && g + u < kItems; ++u) {
+        const int64_t i = base + (int64_t)(g + u) * kThreads;
+        const int64_t ic = i < n ? i : n - 1;
+        if (n > 0) {
+          if constexpr (P12 == 2) {
+            r[u] = k4_ld12(rin, ic);
+          } else {
+            r[u] = ld_rec(ic < split ? rin + ic : rin2 + (ic - split));
+            if constexpr (P12 == 1) r[u] = k4_pack12(r[u], ks.p12cb);
+          }
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < kHistUnroll && g + u < kItems; ++u)
+        if (base + (int64_t)(g + u) * kThreads < n && r[u].pid != kK4EmptyKey)
+          atomicAdd(&st[digit_of(ks, pass, r[u])], 1u);
+    }
+    __syncthreads();
+    tile_cnt[tile * 256 + t] = st[t];
+    st[t] = 0;
+    __syncthreads();
+  }
+}
+
 // Tile-offset scan, step 1: per chunk of kScanTiles tiles, the digit sums.
 constexpr int kScanTiles = 256;
 __global__ __launch_bounds__(kThreads) void k_tile_chunk_sums(const unsigned int* __restrict__ tile_cnt,
@@ -2395,6 +2440,9 @@ int k4_run(pdp_ctx* ctx, hipStream_t stream, const K4Plan& k, const K4Red& kr, b
   const size_t status_bytes = (size_t)tiles * kStatusStride * 8;
   const Rec* src = in_a;
   Rec* dst = buf1;
+  // reduce-then-scan passes (tile digit counts, scanned tile bases, tiles in XCD-contiguous runs) unless
+  // PDP_K4_TILESCAN=0 (decoupled look-back, rounds 3-4)
+  const bool rts = use_tile_scan(total, 0) && env_int("PDP_K4_TILESCAN", 1) != 0;
   {
     ProfScope ps(ctx, PDP_STAGE_PAIR_PASS, stream);
     for (int p = 0; p < k.passes; ++p) {
@@ -2402,14 +2450,25 @@ int k4_run(pdp_ctx* ctx, hipStream_t stream, const K4Plan& k, const K4Red& kr, b
         HIP_TRY(hipMemsetAsync(counters + kCtrTile0, 0, (kNumCounters - kCtrTile0) * 8, stream));
         ctx->tile_slot = kCtrTile0;
       }
-      if (int rc = next_epoch(ctx, stream, status, status_bytes)) return rc;
+      const int n_slot = p == 0 ? (int)kCtrK4In : (int)kCtrK4Pairs;
+      const Rec* src2 = p == 0 ? in_b : (const Rec*)nullptr;
+      const int64_t split = p == 0 ? len_a : (int64_t)INT64_MAX;
+      const unsigned int* bases = nullptr;
+      if (rts) {
+        const TileScan ts = tile_scan_bufs(ctx, status, tiles);
+        auto cnt_kern = !k.p12 ? k_pair_tile_counts<0> : p == 0 ? k_pair_tile_counts<1> : k_pair_tile_counts<2>;
+        hipLaunchKernelGGL(cnt_kern, dim3(grid_for(tiles, 1, 4096)), dim3(kThreads), 0, stream, src, src2, split,
+                           counters, n_slot, ks, p, tiles, ts.tile_cnt);
+        tile_scan(ts, off + p * kHist, stream);
+        bases = ts.tile_cnt;
+      } else if (int rc = next_epoch(ctx, stream, status, status_bytes)) {
+        return rc;
+      }
       auto pass_kern = !k.p12 ? k_pair_pass : p == 0 ? k_pair_pass12_first : k_pair_pass12;
       hipLaunchKernelGGL(pass_kern, dim3((unsigned)tiles), dim3(kThreads), 0, stream, (const int64_t*)nullptr,
-                         (const int64_t*)nullptr, (const double*)nullptr, src, dst, (int64_t)0, counters,
-                         p == 0 ? (int)kCtrK4In : (int)kCtrK4Pairs, ks, p, off + p * kHist, status, ctx->epoch,
-                         counters, (int)ctx->tile_slot++, (const unsigned int*)nullptr, (uint32_t*)nullptr,
-                         (const uint32_t*)nullptr, p == 0 ? in_b : (const Rec*)nullptr,
-                         p == 0 ? len_a : (int64_t)INT64_MAX);
+                         (const int64_t*)nullptr, (const double*)nullptr, src, dst, (int64_t)0, counters, n_slot,
+                         ks, p, off + p * kHist, status, ctx->epoch, counters, (int)ctx->tile_slot++, bases,
+                         (uint32_t*)nullptr, (const uint32_t*)nullptr, src2, split);
       src = dst;
       dst = (dst == buf1) ? buf2 : buf1;
     }
@@ -2635,10 +2694,11 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
                      (int)kCtrNKept);
   Rec* src = nullptr;
   Rec* dst = recs_a;
-  // Passes >= 1 by decoupled look-back: at c4 (3 passes) the look-back passes took 12.28 ms for
-  // two against 10.7 + 3.22 ms with the reduce-then-scan upsweeps (same box).  Pass 0 keeps the
-  // tile counts K0 produces anyway.
-  const bool rest_tile_scan = env_int("PDP_PASS_TILESCAN", 0) != 0;
+  // Passes >= 1 reduce-then-scan too (round 4): at c4 the two later passes took 2 x 5.03 ms by
+  // decoupled look-back against 2 x 3.22 ms + 1.06 ms per pass of tile counts with the XCD-contiguous
+  // tile runs (step 38.31 -> 37.81 ms, same box r04h; round 3, before the loads-ahead passes, had
+  // measured the reverse).  PDP_PASS_TILESCAN=0: look-back.
+  const bool rest_tile_scan = env_int("PDP_PASS_TILESCAN", 1) != 0;
   for (int p = 0; p < ks.passes; ++p) {
     const unsigned int* bases = nullptr;
     if (rts && (p == 0 || rest_tile_scan)) {

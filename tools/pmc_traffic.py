@@ -28,7 +28,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 STAGE_OF = {"k_histogram_tiles": "histogram", "k_bucket_pass": "onesweep_first", "k_sort_first": "onesweep_first",
             "k_filter": "filter", "k_thin": "buckets", "k_lean": "buckets", "k_segments": "buckets",
             "k_segments_big": "buckets", "k4_fill_ranges": "buckets", "k_pair_pass": "pair_pass",
-            "k4_offsets": "pair_pass", "k4_set_counter": "pair_pass", "k4_reduce": "reduce",
+            "k_pair_pass12_first": "pair_pass", "k_pair_pass12": "pair_pass", "k4_offsets": "pair_pass", "k4_set_counter": "pair_pass", "k4_reduce": "reduce",
             "k4_zero_shared": "reduce", "k4_finalize": "reduce", "k_release": "release",
             "k_unpack_counts": "buckets"}
 # kernels of a records radix sort (the survivor sort after k_filter, or a pid-sort pass >= 1)

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Runs on the GPU box (via gpurun).  For each workload W of $PROFILE_WORKLOADS
-# (default "c3 c4"): one bench line (c3 with the CPU baseline), a rocprofv3
+# (default "c3 c4"): one bench line (with the CPU baseline), a rocprofv3
 # kernel-trace/stats pass, one PMC pass per HBM counter (FETCH_SIZE and
 # WRITE_SIZE cannot share a pass on gfx950) and one SQ pass (wave cycles,
 # waits, VALU, occupancy).  Then bench lines + kernel traces of
@@ -23,8 +23,7 @@ run() {  # name timeout cmd...
   return 0
 }
 for w in ${PROFILE_WORKLOADS:-c3 c4}; do
-  cpu=""; [ "$w" != "c3" ] && cpu="--no-cpu-baseline"
-  run "bench_$w" 420 python -u bench.py --workload $w $cpu "$@"
+  run "bench_$w" 420 python -u bench.py --workload $w "$@"
   tail -1 "$O/bench_$w.out" | cut -c1-300
   run "kt_$w" 300 rocprofv3 --kernel-trace --stats -T -f csv -d "$O/kt_$w" -o run -- \
     python -u bench.py --workload $w --steps 5 --warmup 2 --no-cpu-baseline "$@"
@@ -36,7 +35,7 @@ for w in ${PROFILE_WORKLOADS:-c3 c4}; do
     python -u bench.py --workload $w --steps 1 --warmup 1 --no-cpu-baseline --no-profile "$@"
 done
 for w in ${BENCH_WORKLOADS:-c2 c5 c3v}; do
-  run "bench_$w" 300 python -u bench.py --workload $w --no-cpu-baseline "$@"
+  run "bench_$w" 360 python -u bench.py --workload $w "$@"
   tail -1 "$O/bench_$w.out" | cut -c1-300
   run "kt_$w" 300 rocprofv3 --kernel-trace --stats -T -f csv -d "$O/kt_$w" -o run -- \
     python -u bench.py --workload $w --steps 3 --warmup 1 --no-cpu-baseline "$@"
