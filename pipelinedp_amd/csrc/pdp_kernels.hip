@@ -2440,9 +2440,10 @@ int k4_run(pdp_ctx* ctx, hipStream_t stream, const K4Plan& k, const K4Red& kr, b
   const size_t status_bytes = (size_t)tiles * kStatusStride * 8;
   const Rec* src = in_a;
   Rec* dst = buf1;
-  // reduce-then-scan passes (tile digit counts, scanned tile bases, tiles in XCD-contiguous runs) unless
-  // PDP_K4_TILESCAN=0 (decoupled look-back, rounds 3-4)
-  const bool rts = use_tile_scan(total, 0) && env_int("PDP_K4_TILESCAN", 1) != 0;
+  // decoupled look-back passes; PDP_K4_TILESCAN=1: reduce-then-scan (tile digit counts, scanned tile
+  // bases, tiles in XCD-contiguous runs) -- parity-green, but c4 pair passes 8.31 -> 8.60 ms with it
+  // (the counts re-read 8 GB of slots; same box r04i), c3 / c2 unchanged
+  const bool rts = use_tile_scan(total, 0) && env_int("PDP_K4_TILESCAN", 0) != 0;
   {
     ProfScope ps(ctx, PDP_STAGE_PAIR_PASS, stream);
     for (int p = 0; p < k.passes; ++p) {
