@@ -163,7 +163,6 @@ struct KeySpec {
   int ablate;  // kDebugNoLookback / kDebugLinearWrite (timing ablations, results invalid)
   int xcd_remap;  // reduce-then-scan passes: blocks sharing an XCD take one contiguous run of tiles
   int64_t cap;  // mode 6: records the output holds; a scatter position beyond it is reported, not written
-  int p12cb;    // K4 12-byte pair records: count bits below the partition id in the key (pdp_reduce.inc)
 };
 
 // How a row's value feeds the accumulators (combiners.py:254-261, 305-311,
@@ -188,8 +187,11 @@ struct SegParams {
   // record {pk, count, x} per kept (pid, pk) group into slot k4x[s + i] of its segment [s, s + n)
   // (empty records in the segment's other slots) instead of adding to the accumulators, and
   // counts the records' partition-block digits in k4hist; VARIANCE writes {pk, 0, y} to k4y.
+  // k4cb >= 0: the slots are the 12-byte records {pk << k4cb | count - 1, x} of the pair passes
+  // (k4_pack12; an empty slot writes only its all-ones key); -1: 16-byte Rec slots.
   Rec* k4x;
   Rec* k4y;
+  int k4cb;
   unsigned int* k4hist;  // [kK4Rep][kK4MaxPasses][256]
   int k4sh;              // partition block = pk >> k4sh
   int k4passes;
@@ -507,9 +509,9 @@ __global__ __launch_bounds__(kThreads) void k_tile_counts(const Rec* __restrict_
 }
 
 // The same for the K4 pair passes (reduce-then-scan instead of decoupled
-// look-back; round 4): records read as the pass reads them (P12 1: 16-B slots
-// packed to 12-byte keys, 2: 12-byte records; pass 0 also reads the generic
-// path's pairs after `split`), empty slots not counted.
+// look-back; round 4): records read as the pass reads them (P12: 12-byte
+// records; pass 0 also reads the generic path's pairs after `split`), empty
+// slots not counted.
 template <int P12>
 __global__ __launch_bounds__(kThreads) void k_pair_tile_counts(const Rec* __restrict__ rin,
                                                                const Rec* __restrict__ rin2, int64_t split,
@@ -531,11 +533,10 @@ __global__ __launch_bounds__(kThreads) void k_pair_tile_counts(const Rec* __rest
         const int64_t i = base + (int64_t)(g + u) * kThreads;
         const int64_t ic = i < n ? i : n - 1;
         if (n > 0) {
-          if constexpr (P12 == 2) {
-            r[u] = k4_ld12(rin, ic);
+          if constexpr (P12 != 0) {
+            r[u] = ic < split ? k4_ld12(rin, ic) : k4_ld12(rin2, ic - split);
           } else {
             r[u] = ld_rec(ic < split ? rin + ic : rin2 + (ic - split));
-            if constexpr (P12 == 1) r[u] = k4_pack12(r[u], ks.p12cb);
           }
         }
       }
@@ -675,8 +676,8 @@ __device__ __forceinline__ uint32_t xcd_tile(uint32_t b, uint32_t nwg) {
   return (x < r ? x * (q + 1u) : r * (q + 1u) + (x - r) * q) + b / 8u;
 }
 
-// P12 (K4 pair passes with 12-byte records, pdp_reduce.inc): 1 = 16-B pair slots {pk, count, x} in,
-// 12-B records {key = pk << cb | count - 1, x} out; 2 = 12-B records in and out.
+// P12 (K4 pair passes with 12-byte records {key = pk << cb | count - 1, x}, pdp_reduce.inc): 12-B
+// records in (K2's slots, then the generic path's pairs after `split`) and out.
 // ANA (with SOA): the utility analysis' first pass -- the columns become the {pk, pid, value} records of
 // ana_rec (k_ana_pack fused in); no row is dropped (out-of-range rows carry the all-ones key).
 template <bool SOA, bool TAG = false, int P12 = 0, bool ANA = false>
@@ -790,11 +791,10 @@ __device__ __forceinline__ void onesweep_body(
     for (int k = g; k < g + kRecGroup && k < kItems; ++k) {
       const int64_t idx = base + k * 64;
       const int64_t ic = full ? idx : (idx < last ? idx : last);
-      if constexpr (P12 == 2) {
-        r[k] = k4_ld12(rin, ic);
+      if constexpr (P12 != 0) {
+        r[k] = ic < split ? k4_ld12(rin, ic) : k4_ld12(rin2, ic - split);
       } else {
         r[k] = ld_rec(ic < split ? rin + ic : rin2 + (ic - split));
-        if constexpr (P12 == 1) r[k] = k4_pack12(r[k], ks.p12cb);
       }
     }
 #pragma unroll
@@ -1036,10 +1036,7 @@ __global__ __launch_bounds__(kThreads, PDP_OS_OCC) void k_bucket_pass(PDP_ONESWE
 __global__ __launch_bounds__(kThreads, PDP_OS_OCC) void k_pair_pass(PDP_ONESWEEP_ARGS) {
   onesweep_body<false, false>(PDP_ONESWEEP_PASS);
 }
-// ... with 12-byte pair records: the first pass (16-B slots in), later passes (12-B in)
-__global__ __launch_bounds__(kThreads, PDP_OS_OCC) void k_pair_pass12_first(PDP_ONESWEEP_ARGS) {
-  onesweep_body<false, false, 1>(PDP_ONESWEEP_PASS);
-}
+// ... with 12-byte pair records (K2 writes its slots in that form)
 __global__ __launch_bounds__(kThreads, PDP_OS_OCC) void k_pair_pass12(PDP_ONESWEEP_ARGS) {
   onesweep_body<false, false, 2>(PDP_ONESWEEP_PASS);
 }
@@ -1740,6 +1737,7 @@ Plan make_plan(int64_t n, int64_t U, int64_t P) {
 
 SegParams make_seg(const pdp_bound_params* bp, int low, int pkb, bool has_value) {
   SegParams sp{};
+  sp.k4cb = -1;
   sp.low = low;
   sp.pkb = pkb;
   sp.seed = bp->sampling_seed;
@@ -2430,7 +2428,6 @@ int k4_run(pdp_ctx* ctx, hipStream_t stream, const K4Plan& k, const K4Red& kr, b
   ks.mode = 6;
   ks.cap = std::min<int64_t>(total, buf_cap);  // the pairs (< total) land in buf1 / buf2
   ks.low = kr.sh + (k.p12 ? k.cb : 0);  // 12-byte records: the block digit sits above the count bits
-  ks.p12cb = k.p12 ? k.cb : 0;
   ks.passes = k.passes;
   for (int i = 0; i < k.passes; ++i) {
     ks.shift[i] = k.shift[i];
@@ -2457,7 +2454,7 @@ int k4_run(pdp_ctx* ctx, hipStream_t stream, const K4Plan& k, const K4Red& kr, b
       const unsigned int* bases = nullptr;
       if (rts) {
         const TileScan ts = tile_scan_bufs(ctx, status, tiles);
-        auto cnt_kern = !k.p12 ? k_pair_tile_counts<0> : p == 0 ? k_pair_tile_counts<1> : k_pair_tile_counts<2>;
+        auto cnt_kern = k.p12 ? k_pair_tile_counts<1> : k_pair_tile_counts<0>;
         hipLaunchKernelGGL(cnt_kern, dim3(grid_for(tiles, 1, 4096)), dim3(kThreads), 0, stream, src, src2, split,
                            counters, n_slot, ks, p, tiles, ts.tile_cnt);
         tile_scan(ts, off + p * kHist, stream);
@@ -2465,7 +2462,7 @@ int k4_run(pdp_ctx* ctx, hipStream_t stream, const K4Plan& k, const K4Red& kr, b
       } else if (int rc = next_epoch(ctx, stream, status, status_bytes)) {
         return rc;
       }
-      auto pass_kern = !k.p12 ? k_pair_pass : p == 0 ? k_pair_pass12_first : k_pair_pass12;
+      auto pass_kern = k.p12 ? k_pair_pass12 : k_pair_pass;
       hipLaunchKernelGGL(pass_kern, dim3((unsigned)tiles), dim3(kThreads), 0, stream, (const int64_t*)nullptr,
                          (const int64_t*)nullptr, (const double*)nullptr, src, dst, (int64_t)0, counters, n_slot,
                          ks, p, off + p * kHist, status, ctx->epoch, counters, (int)ctx->tile_slot++, bases,
@@ -2594,6 +2591,7 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
     q.k4y = k4y;
     q.k4hist = k4rep;
     q.k4sh = k4.sh;
+    q.k4cb = k4.p12 ? k4.cb : -1;
     q.k4passes = k4.passes;
     for (int i = 0; i < kK4MaxPasses; ++i) {
       q.k4shift[i] = k4.shift[i];
