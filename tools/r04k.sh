@@ -8,4 +8,4 @@ mkdir -p "$O"
 tools/gpu_check.sh "$N" "tests -m gpu" "" || exit $?
 grep -q " passed" "$O/tests.log" && ! grep -q " failed" "$O/tests.log" || { echo "tests failed"; exit 1; }
 tools/envexp.sh "$N" 'c4 -- --workload c4' 'c4p16 PDP_K4_P12=0 -- --workload c4' 'c4b -- --workload c4' \
-  'c3v -- --workload c3v' 'c3vp16 PDP_K4_P12=0 -- --workload c3v' 'c3 -- --workload c3' || exit $?
+  'c4i4 PDP_HIP_LIB=variants/lib_k4i4.so -- --workload c4' 'c3v -- --workload c3v' 'c3vp16 PDP_K4_P12=0 -- --workload c3v' 'c3 -- --workload c3' || exit $?
