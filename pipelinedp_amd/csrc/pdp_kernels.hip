@@ -342,6 +342,9 @@ __device__ __forceinline__ T block_max(T v, T* s_tmp) {
 #ifndef PDP_HIST_NT
 #define PDP_HIST_NT 1  // non-temporal column loads in k_histogram_tiles (c3 K0 1.60 -> 1.49 ms, r04b)
 #endif
+#ifndef PDP_HIST_V2
+#define PDP_HIST_V2 1  // k_histogram_tiles: 16-byte column loads (two rows per lane) for full, aligned tiles
+#endif
 constexpr int kHistUnroll = PDP_HIST_UNROLL;  // rows per thread with loads in flight together (K0, K1u)
 
 // Utility-analysis record of a row (k_ana_pack restated for the fused first pass):
@@ -428,9 +431,47 @@ __global__ __launch_bounds__(kThreads) void k_histogram_tiles(const int64_t* __r
   __syncthreads();
   unsigned int invalid = 0;
   const int64_t tiles = (n + kTile - 1) / kTile;
+  // 16-byte loads (two rows per lane, PDP_HIST_V2) need 16-byte aligned columns
+  const bool v2 = PDP_HIST_V2 && ((reinterpret_cast<uintptr_t>(pid) | (PID_ONLY ? 0 : reinterpret_cast<uintptr_t>(pk))) & 15) == 0;
+  auto count_row = [&](int64_t a, int64_t b) {
+    if (b < 0 || b >= (int64_t)ks.num_parts || a < 0 || a >= (int64_t)ks.num_pids) {
+      if (b >= 0) ++invalid;
+      atomicAdd(&sh[256], 1u);
+      return;
+    }
+    Rec r;
+    r.pid = (uint32_t)a;
+    r.pk = (uint32_t)b;
+    r.val = 0.0;
+    const uint32_t d0 = digit_of(ks, 0, r);
+    atomicAdd(&sh[d0], 1u);
+    atomicAdd(&st[d0], 1u);
+    for (int p = 1; p < ks.passes; ++p) atomicAdd(&sh[p * kHist + digit_of(ks, p, r)], 1u);
+  };
   for (int64_t tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
     const int64_t base = tile * kTile + t;
     const bool full = (tile + 1) * kTile <= n;
+    if (v2 && full) {  // the tile as kItems / 2 slices of 2 * kThreads rows; lane t reads rows 2t, 2t + 1
+      typedef long long ll2 __attribute__((ext_vector_type(2)));
+      const ll2* pv = reinterpret_cast<const ll2*>(pid + tile * kTile);
+      const ll2* kv = reinterpret_cast<const ll2*>(pk + tile * kTile);
+      ll2 a[kItems / 2], b[kItems / 2];
+#pragma unroll
+      for (int u = 0; u < kItems / 2; ++u) {
+        a[u] = __builtin_nontemporal_load(pv + u * kThreads + t);
+        if (!PID_ONLY) b[u] = __builtin_nontemporal_load(kv + u * kThreads + t);
+      }
+#pragma unroll
+      for (int u = 0; u < kItems / 2; ++u) {
+        count_row(a[u].x, PID_ONLY ? 0 : b[u].x);
+        count_row(a[u].y, PID_ONLY ? 0 : b[u].y);
+      }
+      __syncthreads();
+      tile_cnt[tile * 256 + t] = st[t];
+      st[t] = 0;
+      __syncthreads();
+      continue;
+    }
 #pragma unroll
     for (int g = 0; g < kItems; g += kHistUnroll) {
       int64_t a[kHistUnroll], b[kHistUnroll];
@@ -448,19 +489,7 @@ __global__ __launch_bounds__(kThreads) void k_histogram_tiles(const int64_t* __r
 #pragma unroll
       for (int u = 0; u < kHistUnroll && g + u < kItems; ++u) {
         if (!full && base + (int64_t)(g + u) * kThreads >= n) break;
-        if (b[u] < 0 || b[u] >= (int64_t)ks.num_parts || a[u] < 0 || a[u] >= (int64_t)ks.num_pids) {
-          if (b[u] >= 0) ++invalid;
-          atomicAdd(&sh[256], 1u);
-          continue;
-        }
-        Rec r;
-        r.pid = (uint32_t)a[u];
-        r.pk = (uint32_t)b[u];
-        r.val = 0.0;
-        const uint32_t d0 = digit_of(ks, 0, r);
-        atomicAdd(&sh[d0], 1u);
-        atomicAdd(&st[d0], 1u);
-        for (int p = 1; p < ks.passes; ++p) atomicAdd(&sh[p * kHist + digit_of(ks, p, r)], 1u);
+        count_row(a[u], b[u]);
       }
     }
     __syncthreads();
