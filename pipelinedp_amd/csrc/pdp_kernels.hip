@@ -1986,7 +1986,9 @@ int sort_recs(pdp_ctx* ctx, Rec* a, Rec* b, int64_t m, const KeySpec& ks, unsign
   const bool rts = use_tile_scan(m, 0) && env_int("PDP_SORT_TILESCAN", 0) != 0;
   for (int p = 0; p < ks.passes; ++p) {
     const unsigned int* bases = nullptr;
-    if (rts) {
+    // the fused first pass of the utility analysis reads the SoA columns: its tile counts would need
+    // them too, so it always runs by look-back (k_tile_counts reads records)
+    if (rts && !(soa_pk && p == 0)) {
       const TileScan ts = tile_scan_bufs(ctx, status, tiles);
       hipLaunchKernelGGL(k_tile_counts, dim3(grid_for(tiles, 1, 4096)), dim3(kThreads), 0, stream, src, counters,
                          (int)kCtrNGeneric, ks, p, tiles, ts.tile_cnt);
