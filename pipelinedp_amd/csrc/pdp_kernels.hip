@@ -2400,7 +2400,7 @@ K4Plan k4_plan(const pdp_bound_params* bp, const SegParams& sp, int64_t n, int64
   // the 2048-partition window (56 KiB of LDS: 2 reduce workgroups per CU) unless the 4096 one saves a pass
   auto npasses = [&](int sh) { return (std::max(1, pkb - sh) + 7) / 8; };
   k.sh = npasses(kK4ShMax) < npasses(kK4ShMax - 1) ? kK4ShMax : kK4ShMax - 1;
-  if (const int e = env_int("PDP_K4_SH", 0)) k.sh = std::min(kK4ShMax, std::max(kK4ShMax - 1, e));
+  if (const int e = env_int("PDP_K4_SH", 0)) k.sh = std::min(kK4ShMax, std::max(kK4ShMax - 2, e));
   const int kb = std::max(1, pkb - k.sh);
   k.passes = (kb + 7) / 8;
   int rem = kb, sh = 0;
@@ -2509,13 +2509,17 @@ int k4_run(pdp_ctx* ctx, hipStream_t stream, const K4Plan& k, const K4Red& kr, b
   if (scratch)
     hipLaunchKernelGGL(k.p12 ? k4_zero_shared<1> : k4_zero_shared<0>, dim3((unsigned)(chunks - 1)), dim3(kThreads), 0,
                        stream, src, counters, kr.sh, kr.P, kr.chunk, s_lo, s_hi, s_fl, kr.cb);
+  // window of 2^sh partitions: 12 or 11 by k4_plan, 10 by PDP_K4_SH=10 (28 KiB of LDS: 4 workgroups per CU)
+  auto pick = [&](auto k12, auto k11, auto k10) { return kr.sh == kK4ShMax ? k12 : kr.sh == kK4ShMax - 1 ? k11 : k10; };
   decltype(&k4_reduce<true, kK4ShMax, 0>) kern;
   if (k.p12)
-    kern = y ? (kr.sh == kK4ShMax ? k4_reduce<true, kK4ShMax, 1> : k4_reduce<true, kK4ShMax - 1, 1>)
-             : (kr.sh == kK4ShMax ? k4_reduce<false, kK4ShMax, 1> : k4_reduce<false, kK4ShMax - 1, 1>);
+    kern = y ? pick(k4_reduce<true, kK4ShMax, 1>, k4_reduce<true, kK4ShMax - 1, 1>, k4_reduce<true, kK4ShMax - 2, 1>)
+             : pick(k4_reduce<false, kK4ShMax, 1>, k4_reduce<false, kK4ShMax - 1, 1>,
+                    k4_reduce<false, kK4ShMax - 2, 1>);
   else
-    kern = y ? (kr.sh == kK4ShMax ? k4_reduce<true, kK4ShMax, 0> : k4_reduce<true, kK4ShMax - 1, 0>)
-             : (kr.sh == kK4ShMax ? k4_reduce<false, kK4ShMax, 0> : k4_reduce<false, kK4ShMax - 1, 0>);
+    kern = y ? pick(k4_reduce<true, kK4ShMax, 0>, k4_reduce<true, kK4ShMax - 1, 0>, k4_reduce<true, kK4ShMax - 2, 0>)
+             : pick(k4_reduce<false, kK4ShMax, 0>, k4_reduce<false, kK4ShMax - 1, 0>,
+                    k4_reduce<false, kK4ShMax - 2, 0>);
   hipLaunchKernelGGL(kern, dim3((unsigned)chunks), dim3(kK4Threads), 0, stream, src, counters, kr, acc, s_lo, s_hi,
                      s_fl);
   if (scratch) {
