@@ -3247,7 +3247,7 @@ int analysis_impl(pdp_ctx* ctx, const int64_t* pid, const int64_t* pk, const dou
       const int G = nunits > kAnaFixGroup ? kAnaFixGroup : 0;
       hipLaunchKernelGGL(k_ana_fix, dim3((unsigned)((nunits + 3) / 4), cgroups), dim3(256), 0, stream, ppk, M, ulen,
                          nunits, G, nconf, nb, P, (const double*)lvl[level & 1], lvl[(level + 1) & 1], out->metrics,
-                         mom);
+                         mom, (int)!priv);
       if (G == 0) break;
       nunits = (nunits + G - 1) / G;
       ulen *= G;
