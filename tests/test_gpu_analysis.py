@@ -239,3 +239,36 @@ def test_analysis_sort_forms_bitwise_equal(ex, monkeypatch):
         runs.append((m.cpu().numpy(), prob.cpu().numpy()))
     np.testing.assert_array_equal(runs[0][0], runs[1][0])
     np.testing.assert_array_equal(runs[0][1], runs[1][1])
+
+
+def test_analysis_nonpublic_rows_dropped_and_out_of_range_rejected(ex):
+    """The fused first sort pass packs rows itself (k_histogram<2> / k_ana_sort_first, as k_ana_pack
+    did): rows of non-public partitions (pk < 0) are dropped -- the metrics equal those of the
+    remaining rows bit for bit -- and a partition id >= P or a public row's privacy id >= U is an
+    error, as in the aggregate path."""
+    import torch
+    from pipelinedp_amd import native
+    from pipelinedp_amd.native import NativeError
+    rng = np.random.default_rng(31)
+    n, U, P = 200_000, 5_000, 700
+    pid, pk, val = o.synth_rows(n, U, P, seed=37, zipf_s=1.1, value_lo=-1, value_hi=6)
+    drop = rng.random(n) < 0.3
+    pk_np = pk.copy()
+    pk_np[drop] = -1
+    cfgs = _cfgs(rng, 8, True)
+    mask = native.METRIC_SUM | native.METRIC_COUNT | native.METRIC_PRIVACY_ID_COUNT
+    d = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
+    m1, p1, _ = ex.analyze(d(pid), d(pk_np), d(val), U, P, mask, cfgs)
+    keep = ~drop
+    m2, p2, _ = ex.analyze(d(pid[keep]), d(pk[keep]), d(val[keep]), U, P, mask, cfgs)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(m1.cpu().numpy(), m2.cpu().numpy())
+    np.testing.assert_array_equal(p1.cpu().numpy(), p2.cpu().numpy())
+    bad_pk = pk.copy()
+    bad_pk[123] = P
+    with pytest.raises(NativeError, match="out of range"):
+        ex.analyze(d(pid), d(bad_pk), d(val), U, P, mask, cfgs)
+    bad_pid = pid.copy()
+    bad_pid[456] = U
+    with pytest.raises(NativeError, match="out of range"):
+        ex.analyze(d(bad_pid), d(pk), d(val), U, P, mask, cfgs)
