@@ -90,6 +90,12 @@ struct __align__(16) Rec {
 #ifndef PDP_OS_NT
 #define PDP_OS_NT 0
 #endif
+#ifndef PDP_DIGIT_MODE6_BRANCH
+#define PDP_DIGIT_MODE6_BRANCH 0
+#endif
+#ifndef PDP_SCATTER_CHECK
+#define PDP_SCATTER_CHECK 0
+#endif
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 // 16-byte record load / store of the radix passes (streamed once: optionally
@@ -245,9 +251,18 @@ __device__ __forceinline__ uint32_t digit_of(const KeySpec& ks, int pass, const 
   // the caller (onesweep_body), not here: an extra early-return branch in this
   // chain was miscompiled on gfx950 (ROCm 7.2) -- the mode 1 / 4 digits of the
   // survivor and analysis sorts came out wrong (bisected on MI355X).
+#if PDP_DIGIT_MODE6_BRANCH  // round-3 form, for the miscompile re-check (variant builds only)
+  if (ks.mode == 0) {
+    key = (uint64_t)(r.pid >> ks.low);
+  } else if (ks.mode == 6) {
+    if (r.pid == 0xFFFFFFFFu) return 256u;  // empty slot
+    key = (uint64_t)(r.pid >> ks.low);
+  } else if (ks.mode == 4) {
+#else
   if (ks.mode == 0 || ks.mode == 6) {
     key = (uint64_t)(r.pid >> ks.low);
   } else if (ks.mode == 4) {
+#endif
     if (sh >= 64) return (uint32_t)(((uint64_t)r.pid * ks.mult) >> 32);
     key = (uint64_t)r.pid;
   } else if (ks.mode == 1) {
@@ -1014,6 +1029,12 @@ __device__ __forceinline__ void onesweep_body(
           atomicOr(&counters[kCtrErr], 4ull);
           continue;
         }
+#if PDP_SCATTER_CHECK  // variant builds: every scatter position inside the input's row count
+        if (q < 0 || q >= n_eff) {
+          atomicOr(&counters[kCtrErr], 8ull);
+          continue;
+        }
+#endif
         if constexpr (P12 != 0) k4_st12(rout, q, rc);
         else st_rec(rout + q, rc);
         if constexpr (TAG) tag_out[q] = rc.pid;
