@@ -248,9 +248,10 @@ __device__ __forceinline__ uint32_t digit_of(const KeySpec& ks, int pass, const 
   const int sh = ks.shift[pass];
   uint64_t key;
   // Mode 6 (K4 pair records) keys like mode 0; its empty slots are dropped by
-  // the caller (onesweep_body), not here: an extra early-return branch in this
-  // chain was miscompiled on gfx950 (ROCm 7.2) -- the mode 1 / 4 digits of the
-  // survivor and analysis sorts came out wrong (bisected on MI355X).
+  // the caller (onesweep_body).  Round 3 blamed an early-return branch here for
+  // wrong survivor / analysis sort digits; round 4 re-ran the suites with it
+  // (PDP_DIGIT_MODE6_BRANCH=1): green -- the cause was stale look-back status
+  // words (next_epoch), DESIGN.md 3.1c.
 #if PDP_DIGIT_MODE6_BRANCH  // round-3 form, for the miscompile re-check (variant builds only)
   if (ks.mode == 0) {
     key = (uint64_t)(r.pid >> ks.low);
