@@ -2662,6 +2662,12 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
     ctx->stats.k4_slots = nslots + nkf;
     ctx->stats.k4_passes = k4.passes;
     K4Red krx = k4_red(k4, q, P, false), kry = k4_red(k4, q, P, true);
+    if (!env_int("PDP_K4_CHUNK", 0)) {
+      // records per reduce workgroup: 32768, fewer for small inputs so that the reduction still has
+      // about 1024 workgroups (a rank's share of a multi-GPU step: c3 at 8 GPUs has ~8e6 slots)
+      const int64_t c = std::min<int64_t>(kK4Chunk, std::max<int64_t>(4096, (nslots + nkf) / 1024 / 4096 * 4096));
+      krx.chunk = kry.chunk = c;
+    }
     if (parts) {  // fixed-point export (multi-GPU partials)
       krx.fxh = (long long*)parts->x_hi;
       krx.fxl = (long long*)parts->x_lo;
