@@ -163,3 +163,49 @@ def test_partials_over_emulated_ranks_equal_one_gpu_bitwise(world_size, metrics)
             np.testing.assert_array_equal(a.cpu().numpy(), b.cpu().numpy(), err_msg=name)
     if one.x is not None:
         assert bool(torch.isnan(one.x[5])) and int(torch.isnan(one.x).sum()) == 1
+
+
+def test_partials_with_an_empty_rank_equal_one_gpu_bitwise():
+    """A rank with no rows (possible for small inputs or skewed shards) exports all-zero partials;
+    adding them changes nothing: the merge over [rows of rank 0 | no rows] equals one
+    pdp_bound_accumulate bit for bit, and an all-empty merge finalises to zero accumulators."""
+    import torch
+    from pipelinedp_amd import native
+    from pipelinedp_amd.executor import BoundConfig, HipExecutor, Partials
+    ex = HipExecutor(0)
+    n, U, P = 50000, 2000, 900
+    pid, pk, val = o.synth_rows(n, U, P, seed=41, zipf_s=1.1, value_lo=-2, value_hi=9)
+    M = native
+    cfg = BoundConfig(M.METRIC_COUNT | M.METRIC_MEAN | M.METRIC_VARIANCE, 3, 2, 0.0, 8.0, sampling_seed=5)
+    d = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
+    one = ex.accumulate(d(pid), d(pk), d(val), U, P, cfg)
+    full = ex.accumulate_partials(d(pid), d(pk), d(val), U, P, cfg)
+    e = np.zeros(0, np.int64)
+    empty = ex.accumulate_partials(d(e), d(e), d(np.zeros(0)), U, P, cfg)
+    torch.cuda.synchronize()
+    assert int(empty.data.abs().sum()) == 0
+    acc = ex.finalize_partials(Partials(full.data + empty.data, full.fields, P), cfg)
+    zero = ex.finalize_partials(Partials(empty.data.clone(), empty.fields, P), cfg)
+    torch.cuda.synchronize()
+    for name in ("row_count", "count", "x", "y"):
+        a, b = getattr(one, name), getattr(acc, name)
+        np.testing.assert_array_equal(a.cpu().numpy(), b.cpu().numpy(), err_msg=name)
+        assert float(getattr(zero, name).abs().sum()) == 0.0, name
+
+
+def test_analysis_of_no_rows():
+    """An empty input through the utility analysis: every partition has no privacy ids, the keep
+    probability is 0 and the metrics are the empty accumulators'."""
+    import torch
+    from pipelinedp_amd import native
+    from pipelinedp_amd.executor import HipExecutor
+    ex = HipExecutor(0)
+    e = np.zeros(0, np.int64)
+    cfg = native.AnalysisConfig(2, 1, 0.0, 5.0, native.SELECTION_TRUNCATED_GEOMETRIC, 0, 1.0, 1e-5)
+    mask = native.METRIC_SUM | native.METRIC_COUNT | native.METRIC_PRIVACY_ID_COUNT
+    d = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
+    m, prob, pids = ex.analyze(d(e), d(e), d(np.zeros(0)), 10, 7, mask, [cfg])
+    torch.cuda.synchronize()
+    assert float(prob.abs().sum()) == 0.0
+    assert int(pids.sum()) == 0
+    assert float(m.abs().sum()) == 0.0
