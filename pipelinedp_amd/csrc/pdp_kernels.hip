@@ -3175,6 +3175,9 @@ int analysis_impl(pdp_ctx* ctx, const int64_t* pid, const int64_t* pk, const dou
   const size_t status_bytes = (size_t)L.tiles * kStatusStride * 8;
   const int pkbits = std::max(1, pdp::ceil_log2_u64((uint64_t)P + 1));
   int64_t M = 0;
+  bool np_hist = false;
+  int np_sh = 0;
+  uint32_t* np_spare = nullptr;
   if (n > 0) {
     ProfScope ps(ctx, PDP_STAGE_ANALYSIS_PAIRS, stream);
     const int g = grid_for(n, kThreads, 8192);
@@ -3203,8 +3206,12 @@ int analysis_impl(pdp_ctx* ctx, const int64_t* pid, const int64_t* pk, const dou
         const int64_t tiles = (n + kAnaTile - 1) / kAnaTile;
         hipLaunchKernelGGL(k_ana_tile_groups, dim3((unsigned)tiles), dim3(256), 0, stream, sorted, n, flags);
         if (int rc = scan_inplace(flags, tiles, stream)) return rc;
+        // n_partitions of the sampled pairs: bucketed LDS histogram (np_hist) or one atomic per pair
+        np_sh = std::max(0, pidbits - 8);
+        np_hist = np_sh <= 14 && env_int("PDP_ANA_NPART_HIST", 0);
+        np_spare = (uint32_t*)(sorted == ra ? rb : ra);
         hipLaunchKernelGGL(k_ana_tile_pairs, dim3((unsigned)tiles), dim3(256), 0, stream, sorted, n, flags, num_sampled,
-                           ppk, pref, pcnt, psum, npart, counters);
+                           ppk, pref, pcnt, psum, npart, counters, (int)!np_hist);
       }
     } else {
       // pre-aggregated pairs -> sorted by pk
@@ -3232,6 +3239,20 @@ int analysis_impl(pdp_ctx* ctx, const int64_t* pid, const int64_t* pk, const dou
     if (host_ctr[kCtrErr]) return fail(PDP_ERR_INTERNAL, "radix look-back timed out");
     if (host_ctr[kCtrInvalid]) return fail(PDP_ERR_OUT_OF_RANGE, "privacy id or partition id out of range");
     M = (int64_t)host_ctr[kCtrAnaPairs];
+    if (np_hist && M > 0) {
+      // hist[0, 256): bucket counts, off[0, 256): cursors, off[256, 513): bucket starts (zeroed above)
+      unsigned long long* bcnt = hist;
+      unsigned long long* cur = off;
+      unsigned long long* beg = off + kNpBuckets;
+      const unsigned nt = (unsigned)((M + kNpTile - 1) / kNpTile);
+      HIP_TRY(hipMemsetAsync(bcnt, 0, kNpBuckets * 8, stream));
+      hipLaunchKernelGGL(k_np_bucket_count, dim3(nt), dim3(256), 0, stream, pref, M, np_sh, bcnt);
+      hipLaunchKernelGGL(k_np_bucket_scan, dim3(1), dim3(256), 0, stream, bcnt, cur, beg);
+      hipLaunchKernelGGL(k_np_bucket_scatter, dim3(nt), dim3(256), 0, stream, pref, M, np_sh, cur, np_spare);
+      hipLaunchKernelGGL(k_np_bucket_hist, dim3(kNpBuckets), dim3(1024), (size_t)4 << np_sh, stream, np_spare, beg,
+                         np_sh, U, npart);
+      HIP_TRY(hipGetLastError());
+    }
   }
   ctx->stats.kept_rows_in = M;  // pairs of sampled partitions
   if (pairs_out) {

@@ -241,6 +241,32 @@ def test_analysis_sort_forms_bitwise_equal(ex, monkeypatch):
     np.testing.assert_array_equal(runs[0][1], runs[1][1])
 
 
+def test_analysis_npart_forms_bitwise_equal(ex, monkeypatch):
+    """n_partitions per privacy id from one atomic per pair (default) or from the bucketed LDS
+    histogram of the sampled pairs' ids (PDP_ANA_NPART_HIST=1; the pairs of partitions that are
+    not sampled keep their atomics): identical metrics, keep probabilities and exported pairs,
+    with all partitions sampled and with a third of them."""
+    import torch
+    from pipelinedp_amd import native
+    rng = np.random.default_rng(41)
+    n, U, P = 500_000, 70_000, 2_000
+    pid, pk, val = o.synth_rows(n, U, P, seed=43, zipf_s=1.1, value_lo=-2, value_hi=8)
+    cfgs = _cfgs(rng, 16, True)
+    mask = native.METRIC_SUM | native.METRIC_COUNT | native.METRIC_PRIVACY_ID_COUNT
+    d = lambda a: torch.from_numpy(a).cuda()  # noqa: E731
+    for ns in (None, P // 3):
+        runs = []
+        for form in ("0", "1"):
+            monkeypatch.setenv("PDP_ANA_NPART_HIST", form)
+            m, prob, ids = ex.analyze(d(pid), d(pk), d(val), U, P, mask, cfgs, num_sampled_partitions=ns)
+            pairs = ex.preaggregate(d(pid), d(pk), d(val), U, P, num_sampled_partitions=ns)
+            torch.cuda.synchronize()
+            runs.append([m.cpu().numpy(), prob.cpu().numpy(), ids.cpu().numpy()] +
+                        [t.cpu().numpy() for t in pairs])
+        for a, b in zip(runs[0], runs[1]):
+            np.testing.assert_array_equal(a, b)
+
+
 def test_analysis_nonpublic_rows_dropped_and_out_of_range_rejected(ex):
     """The fused first sort pass packs rows itself (k_histogram<2> / k_ana_sort_first, as k_ana_pack
     did): rows of non-public partitions (pk < 0) are dropped -- the metrics equal those of the
