@@ -3208,7 +3208,7 @@ int analysis_impl(pdp_ctx* ctx, const int64_t* pid, const int64_t* pk, const dou
         if (int rc = scan_inplace(flags, tiles, stream)) return rc;
         // n_partitions of the sampled pairs: bucketed LDS histogram (np_hist) or one atomic per pair
         np_sh = std::max(0, pidbits - 8);
-        np_hist = np_sh <= 14 && env_int("PDP_ANA_NPART_HIST", 0);
+        np_hist = np_sh <= 14 && env_int("PDP_ANA_NPART_HIST", 1);
         np_spare = (uint32_t*)(sorted == ra ? rb : ra);
         hipLaunchKernelGGL(k_ana_tile_pairs, dim3((unsigned)tiles), dim3(256), 0, stream, sorted, n, flags, num_sampled,
                            ppk, pref, pcnt, psum, npart, counters, (int)!np_hist);
