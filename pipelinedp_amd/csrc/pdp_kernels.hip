@@ -144,6 +144,9 @@ __device__ __forceinline__ Rec k4_ld12(const Rec* base, int64_t i) {
   r.val = __longlong_as_double((long long)(((uint64_t)p[2] << 32) | p[1]));
   return r;
 }
+// split slots (SegParams.k4soa): the key array, then the values; the offset keeps the values 16-B aligned
+// and inside a buffer of 16 bytes per slot (at most 12 n + 12 bytes)
+inline int64_t k4_soa_offset(int64_t nslots) { return (std::max<int64_t>(nslots, 1) * 4 + 15) / 16 * 16; }
 __device__ __forceinline__ void k4_st12(Rec* base, int64_t i, const Rec& r) {
   uint32_t* p = reinterpret_cast<uint32_t*>(base) + 3 * i;
   const uint64_t b = (uint64_t)__double_as_longlong(r.val);
@@ -169,6 +172,9 @@ struct KeySpec {
   int ablate;  // kDebugNoLookback / kDebugLinearWrite (timing ablations, results invalid)
   int xcd_remap;  // reduce-then-scan passes: blocks sharing an XCD take one contiguous run of tiles
   int64_t cap;  // mode 6: records the output holds; a scatter position beyond it is reported, not written
+  // mode 6, first pass of k_pair_pass12s: the slots are split (keys u32[], then values f64[] at these byte
+  // offsets from rin / rin2), so an empty slot costs its 4-byte key
+  int64_t soa_a, soa_b;
 };
 
 // How a row's value feeds the accumulators (combiners.py:254-261, 305-311,
@@ -198,6 +204,9 @@ struct SegParams {
   Rec* k4x;
   Rec* k4y;
   int k4cb;
+  // k4cb >= 0 and k4soa > 0: split slots instead -- keys u32[slot] at k4x / k4y and the values f64[slot]
+  // k4soa bytes further (k4_soa_offset), so the first pair pass reads 4 bytes of an empty slot, not 12
+  int64_t k4soa;
   unsigned int* k4hist;  // [kK4Rep][kK4MaxPasses][256]
   int k4sh;              // partition block = pk >> k4sh
   int k4passes;
@@ -836,10 +845,25 @@ __device__ __forceinline__ void onesweep_body(
     for (int k = g; k < g + kRecGroup && k < kItems; ++k) {
       const int64_t idx = base + k * 64;
       const int64_t ic = full ? idx : (idx < last ? idx : last);
-      if constexpr (P12 != 0) {
+      if constexpr (P12 == 3) {  // split slots: keys first, all in flight
+        r[k].pid = ic < split ? reinterpret_cast<const uint32_t*>(rin)[ic]
+                              : reinterpret_cast<const uint32_t*>(rin2)[ic - split];
+        r[k].pk = 0u;
+      } else if constexpr (P12 != 0) {
         r[k] = ic < split ? k4_ld12(rin, ic) : k4_ld12(rin2, ic - split);
       } else {
         r[k] = ld_rec(ic < split ? rin + ic : rin2 + (ic - split));
+      }
+    }
+    if constexpr (P12 == 3) {  // ... then the values of the non-empty slots
+#pragma unroll
+      for (int k = g; k < g + kRecGroup && k < kItems; ++k) {
+        const int64_t idx = base + k * 64;
+        const int64_t ic = full ? idx : (idx < last ? idx : last);
+        const double* vp = ic < split ? reinterpret_cast<const double*>(reinterpret_cast<const char*>(rin) + ks.soa_a) + ic
+                                      : reinterpret_cast<const double*>(reinterpret_cast<const char*>(rin2) + ks.soa_b) +
+                                            (ic - split);
+        r[k].val = r[k].pid != kK4EmptyKey ? *vp : 0.0;
       }
     }
 #pragma unroll
@@ -1090,6 +1114,10 @@ __global__ __launch_bounds__(kThreads, PDP_OS_OCC) void k_pair_pass(PDP_ONESWEEP
 // ... with 12-byte pair records (K2 writes its slots in that form)
 __global__ __launch_bounds__(kThreads, PDP_OS_OCC) void k_pair_pass12(PDP_ONESWEEP_ARGS) {
   onesweep_body<false, false, 2>(PDP_ONESWEEP_PASS);
+}
+// ... whose first pass reads K2's split slots (keys, then the values of the non-empty ones)
+__global__ __launch_bounds__(kThreads, PDP_OS_OCC) void k_pair_pass12s(PDP_ONESWEEP_ARGS) {
+  onesweep_body<false, false, 3>(PDP_ONESWEEP_PASS);
 }
 
 // ---------------------------------------------------------------------------
@@ -2151,9 +2179,11 @@ int run_generic(pdp_ctx* ctx, const Rec* sorted, Rec* spare, Rec* alt, const std
                      (int64_t)sp.l0, (uint8_t*)nullptr, grank);
   // 4) kept groups: sums of the kept rows, then accumulators / pair records.
   if (sp.k4x) {
-    HIP_TRY(keep->alloc((void**)&sp.k4x, (size_t)ngroups * sizeof(Rec)));
+    // 16 bytes per group also hold split slots (k4_soa_offset(ngroups) + 8 ngroups <= 12 ngroups + 12)
+    HIP_TRY(keep->alloc((void**)&sp.k4x, (size_t)ngroups * sizeof(Rec) + 16));
     sp.k4y = nullptr;
-    if (sp.want_y) HIP_TRY(keep->alloc((void**)&sp.k4y, (size_t)ngroups * sizeof(Rec)));
+    if (sp.want_y) HIP_TRY(keep->alloc((void**)&sp.k4y, (size_t)ngroups * sizeof(Rec) + 16));
+    if (sp.k4soa) sp.k4soa = k4_soa_offset(ngroups);
     *kf_x = sp.k4x;
     *kf_y = sp.k4y;
     *kf_n = ngroups;
@@ -2402,6 +2432,7 @@ struct K4Plan {
   int fx, fy;  // fixed-point exponents: q = rint(x * 2^f)
   int cb;      // count bits of a 12-byte pair record's key
   bool p12;    // pair passes move 12-byte records {pk << cb | count - 1, x} (pk and count fit 31 bits)
+  bool soa;    // (p12) K2 writes split slots (keys, values); the first pass reads a 4-byte key per empty slot
 };
 
 // F = 62 - ceil(log2 M): |q| <= 2^62 for |x| <= M; sums of < 2^32 records stay exact in (lo, hi).
@@ -2448,6 +2479,8 @@ K4Plan k4_plan(const pdp_bound_params* bp, const SegParams& sp, int64_t n, int64
   // is the group's row count, unbounded), so the key carries no count bits
   k.cb = sp.want_count ? pdp::ceil_log2_u64((uint64_t)std::max(1.0, linf)) : 0;
   k.p12 = pkb + k.cb <= 31 && env_int("PDP_K4_P12", 1) != 0;
+  // split slots: look-back passes only (k_pair_tile_counts reads 12-byte slots)
+  k.soa = k.p12 && env_int("PDP_K4_SOA", 1) != 0 && env_int("PDP_K4_TILESCAN", 0) == 0;
   return k;
 }
 
@@ -2471,7 +2504,8 @@ K4Red k4_red(const K4Plan& k, const SegParams& sp, int64_t P, bool y) {
 int k4_run(pdp_ctx* ctx, hipStream_t stream, const K4Plan& k, const K4Red& kr, bool y, const Rec* in_a,
            int64_t len_a, const Rec* in_b, int64_t len_b, Rec* buf1, Rec* buf2, AccPtrs acc,
            unsigned long long* off, unsigned long long* counters, unsigned long long* status, void* ws,
-           unsigned long long* s_lo, unsigned long long* s_hi, unsigned int* s_fl, int64_t buf_cap) {
+           unsigned long long* s_lo, unsigned long long* s_hi, unsigned int* s_fl, int64_t buf_cap,
+           int64_t soa_a = 0, int64_t soa_b = 0) {
   const int64_t total = len_a + len_b;
   if (total == 0) return 0;
   hipLaunchKernelGGL(k4_set_counter, dim3(1), dim3(64), 0, stream, counters, (int)kCtrK4In,
@@ -2480,6 +2514,8 @@ int k4_run(pdp_ctx* ctx, hipStream_t stream, const K4Plan& k, const K4Red& kr, b
   ks.xcd_remap = env_int("PDP_XCD_REMAP", 1);
   ks.mode = 6;
   ks.cap = std::min<int64_t>(total, buf_cap);  // the pairs (< total) land in buf1 / buf2
+  ks.soa_a = soa_a;
+  ks.soa_b = soa_b;
   ks.low = kr.sh + (k.p12 ? k.cb : 0);  // 12-byte records: the block digit sits above the count bits
   ks.passes = k.passes;
   for (int i = 0; i < k.passes; ++i) {
@@ -2515,7 +2551,7 @@ int k4_run(pdp_ctx* ctx, hipStream_t stream, const K4Plan& k, const K4Red& kr, b
       } else if (int rc = next_epoch(ctx, stream, status, status_bytes)) {
         return rc;
       }
-      auto pass_kern = k.p12 ? k_pair_pass12 : k_pair_pass;
+      auto pass_kern = k.p12 ? (p == 0 && k.soa ? k_pair_pass12s : k_pair_pass12) : k_pair_pass;
       hipLaunchKernelGGL(pass_kern, dim3((unsigned)tiles), dim3(kThreads), 0, stream, (const int64_t*)nullptr,
                          (const int64_t*)nullptr, (const double*)nullptr, src, dst, (int64_t)0, counters, n_slot,
                          ks, p, off + p * kHist, status, ctx->epoch, counters, (int)ctx->tile_slot++, bases,
@@ -2649,6 +2685,7 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
     q.k4hist = k4rep;
     q.k4sh = k4.sh;
     q.k4cb = k4.p12 ? k4.cb : -1;
+    q.k4soa = k4.soa ? k4_soa_offset(n) : 0;  // slot indices < n (sorted rows / survivors / rows)
     q.k4passes = k4.passes;
     for (int i = 0; i < kK4MaxPasses; ++i) {
       q.k4shift[i] = k4.shift[i];
@@ -2678,12 +2715,13 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
       kry.fxn = (unsigned long long*)parts->nan;
       kry.nan_inc = 1ull << 32;
     }
+    const int64_t soa_a = q.k4soa, soa_b = k4.soa ? k4_soa_offset(nkf) : 0;
     if (int rc = k4_run(ctx, stream, k4, krx, false, slots, nslots, kfx, nkf, buf1, buf2, acc, off, counters, status,
-                        workspace, k4lo, k4hi, k4fl, n))
+                        workspace, k4lo, k4hi, k4fl, n, soa_a, soa_b))
       return rc;
     if (q.want_y) {
       if (int rc = k4_run(ctx, stream, k4, kry, true, k4y, nslots, kfy, nkf, buf1, buf2, acc, off, counters, status,
-                          workspace, k4lo, k4hi, k4fl, n))
+                          workspace, k4lo, k4hi, k4fl, n, soa_a, soa_b))
         return rc;
     }
     return 0;

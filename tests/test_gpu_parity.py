@@ -593,22 +593,26 @@ def test_heavy_single_group_generic_path(ex):
 def test_k4_pair_record_forms_bitwise_equal(ex, cfgi, monkeypatch):
     """K4's pair passes move 12-byte records {pk << cb | count - 1, x} when the
     partition id and count fit 31 bits, 16-byte {pk, count, x} otherwise
-    (PDP_K4_P12=0 forces them): the fixed-point sums are integers, so both
-    forms give identical accumulators, sums included."""
+    (PDP_K4_P12=0 forces them); K2 writes the 12-byte form as split slots (keys,
+    then values: the first pass reads 4 bytes of an empty slot) unless
+    PDP_K4_SOA=0: the fixed-point sums are integers, so all three forms give
+    identical accumulators, sums included."""
     n, U, P, z, L0, Linf, vb, pb, mask = CONFIGS[cfgi]
     pid, pk, val = o.synth_rows(n, U, P, seed=700 + cfgi, zipf_s=z, value_lo=-5, value_hi=15)
     bp = o.BoundParams(L0, Linf, *(vb or (None, None)), *(pb or (None, None)))
     need_val = bool(mask & (2 | 4 | 8))
     runs = []
-    for p12 in ("1", "0"):
+    for p12, soa in (("1", "1"), ("1", "0"), ("0", "1")):
         monkeypatch.setenv("PDP_K4_P12", p12)
+        monkeypatch.setenv("PDP_K4_SOA", soa)
         _, _, rc, cnt, x, y = run_gpu(ex, pid, pk, val if need_val else None, U, P, bp, mask, seed=5 + cfgi)
         runs.append((rc, cnt, x, y))
-    for a, b in zip(*runs):
-        if a is None:
-            assert b is None
-        else:
-            np.testing.assert_array_equal(a, b)
+    for other in runs[1:]:
+        for a, b in zip(runs[0], other):
+            if a is None:
+                assert b is None
+            else:
+                np.testing.assert_array_equal(a, b)
 
 
 @pytest.mark.parametrize("p12", ["1", "0"])
