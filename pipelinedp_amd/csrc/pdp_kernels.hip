@@ -2479,8 +2479,10 @@ K4Plan k4_plan(const pdp_bound_params* bp, const SegParams& sp, int64_t n, int64
   // is the group's row count, unbounded), so the key carries no count bits
   k.cb = sp.want_count ? pdp::ceil_log2_u64((uint64_t)std::max(1.0, linf)) : 0;
   k.p12 = pkb + k.cb <= 31 && env_int("PDP_K4_P12", 1) != 0;
-  // split slots: look-back passes only (k_pair_tile_counts reads 12-byte slots)
-  k.soa = k.p12 && env_int("PDP_K4_SOA", 1) != 0 && env_int("PDP_K4_TILESCAN", 0) == 0;
+  // split slots (PDP_K4_SOA=1; parity-green): look-back passes only (k_pair_tile_counts reads 12-byte
+  // slots).  Off: c4 pair passes 8.40 / 8.63 ms against 8.35 / 8.34 with 12-byte slots, c3 0.65 against
+  // 0.62 (the values wait for their keys), for 1 % fewer pair-pass bytes (r04z7)
+  k.soa = k.p12 && env_int("PDP_K4_SOA", 0) != 0 && env_int("PDP_K4_TILESCAN", 0) == 0;
   return k;
 }
 
