@@ -3334,7 +3334,7 @@ int analysis_impl(pdp_ctx* ctx, const int64_t* pid, const int64_t* pk, const dou
     int64_t nunits = waves, ulen = chunk;
     for (int level = 0;; ++level) {
       const int G = nunits > kAnaFixGroup ? kAnaFixGroup : 0;
-      hipLaunchKernelGGL(k_ana_fix, dim3((unsigned)((nunits + 3) / 4), cgroups), dim3(256), 0, stream, ppk, M, ulen,
+      hipLaunchKernelGGL(k_ana_fix, dim3((unsigned)((nunits + 3) / 4), cgroups), dim3(256), 0, stream, ppk, pbeg, M, ulen,
                          nunits, G, nconf, nb, P, (const double*)lvl[level & 1], lvl[(level + 1) & 1], out->metrics,
                          mom, (int)!priv);
       if (G == 0) break;
