@@ -3328,14 +3328,14 @@ int analysis_impl(pdp_ctx* ctx, const int64_t* pid, const int64_t* pk, const dou
     }
     double* slots = (double*)(ws + L.slots);
     hipLaunchKernelGGL(km, dim3((unsigned)((waves + 3) / 4), cgroups), dim3(256), 0, stream, ppk, pref, pcnt, psum,
-                       npart, M, cfg_d, nconf, mflags, P, out->metrics, mom, slots, chunk, (int)!priv, pbeg);
+                       npart, M, cfg_d, nconf, mflags, P, out->metrics, mom, slots, chunk, (int)!priv);
     // fixed-order merge of the chunk-boundary partials, by levels of kAnaFixGroup units
     double* lvl[2] = {slots, (double*)(ws + L.slots2)};
     int64_t nunits = waves, ulen = chunk;
     for (int level = 0;; ++level) {
       const int G = nunits > kAnaFixGroup ? kAnaFixGroup : 0;
       hipLaunchKernelGGL(k_ana_fix, dim3((unsigned)((nunits + 3) / 4), cgroups), dim3(256), 0, stream, ppk, pbeg, M, ulen,
-                         chunk, nunits, G, nconf, nb, P, (const double*)lvl[level & 1], lvl[(level + 1) & 1], out->metrics,
+                         nunits, G, nconf, nb, P, (const double*)lvl[level & 1], lvl[(level + 1) & 1], out->metrics,
                          mom, (int)!priv);
       if (G == 0) break;
       nunits = (nunits + G - 1) / G;
