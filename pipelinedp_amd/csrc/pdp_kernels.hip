@@ -367,6 +367,9 @@ __device__ __forceinline__ T block_max(T v, T* s_tmp) {
 #ifndef PDP_HIST_NT
 #define PDP_HIST_NT 1  // non-temporal column loads in k_histogram_tiles (c3 K0 1.60 -> 1.49 ms, r04b)
 #endif
+#ifndef PDP_HIST_V3
+#define PDP_HIST_V3 1  // k_histogram_tiles<PID_ONLY>: one LDS atomic per row (the histogram adds the tile counts)
+#endif
 #ifndef PDP_HIST_V2
 #define PDP_HIST_V2 1  // k_histogram_tiles: 16-byte column loads (two rows per lane) for full, aligned tiles
 #endif
@@ -448,10 +451,12 @@ __global__ __launch_bounds__(kThreads) void k_histogram_tiles(const int64_t* __r
                                                               KeySpec ks, unsigned long long* __restrict__ hist,
                                                               unsigned int* __restrict__ tile_cnt,
                                                               unsigned long long* __restrict__ counters) {
-  __shared__ unsigned int sh[kMaxPasses * kHist];
+  // PID_ONLY (the pre-filter's bucket digit): one pass, so the histogram is the sum of the tile counts
+  constexpr bool kFromTiles = PID_ONLY && PDP_HIST_V3;
+  __shared__ unsigned int sh[(kFromTiles ? 1 : kMaxPasses) * kHist];
   __shared__ unsigned int st[256];
   const int t = threadIdx.x;
-  for (int i = t; i < kMaxPasses * kHist; i += kThreads) sh[i] = 0;
+  for (int i = t; i < (kFromTiles ? 1 : kMaxPasses) * kHist; i += kThreads) sh[i] = 0;
   st[t] = 0;
   __syncthreads();
   unsigned int invalid = 0;
@@ -469,9 +474,11 @@ __global__ __launch_bounds__(kThreads) void k_histogram_tiles(const int64_t* __r
     r.pk = (uint32_t)b;
     r.val = 0.0;
     const uint32_t d0 = digit_of(ks, 0, r);
-    atomicAdd(&sh[d0], 1u);
     atomicAdd(&st[d0], 1u);
-    for (int p = 1; p < ks.passes; ++p) atomicAdd(&sh[p * kHist + digit_of(ks, p, r)], 1u);
+    if constexpr (!kFromTiles) {
+      atomicAdd(&sh[d0], 1u);
+      for (int p = 1; p < ks.passes; ++p) atomicAdd(&sh[p * kHist + digit_of(ks, p, r)], 1u);
+    }
   };
   for (int64_t tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
     const int64_t base = tile * kTile + t;
@@ -493,6 +500,7 @@ __global__ __launch_bounds__(kThreads) void k_histogram_tiles(const int64_t* __r
       }
       __syncthreads();
       tile_cnt[tile * 256 + t] = st[t];
+      if (kFromTiles) sh[t] += st[t];
       st[t] = 0;
       __syncthreads();
       continue;
@@ -519,10 +527,11 @@ __global__ __launch_bounds__(kThreads) void k_histogram_tiles(const int64_t* __r
     }
     __syncthreads();
     tile_cnt[tile * 256 + t] = st[t];
+    if (kFromTiles) sh[t] += st[t];
     st[t] = 0;
     __syncthreads();
   }
-  for (int i = t; i < ks.passes * kHist; i += kThreads)
+  for (int i = t; i < (kFromTiles ? 1 : ks.passes) * kHist; i += kThreads)
     if (sh[i]) atomicAdd(&hist[i], (unsigned long long)sh[i]);
   if (invalid) atomicAdd(&counters[kCtrInvalid], (unsigned long long)invalid);
 }
