@@ -116,7 +116,7 @@ typedef struct pdp_bound_params {
   uint64_t sampling_seed;                   /* keys the uniform sampling permutations */
   int32_t debug_force_fallback;             /* testing: route every bucket through the
                                                generic sorted-stream path */
-  int32_t reserved;
+  int32_t reserved;                         /* testing: debug flags (pdp_ctx_set_debug); 0 */
 } pdp_bound_params;
 
 /* Dense per-partition accumulators [num_partitions] (device).  row_count is the
@@ -159,6 +159,13 @@ const char* pdp_last_error(void);
 
 pdp_ctx* pdp_ctx_create(int device);
 void pdp_ctx_destroy(pdp_ctx* ctx);
+
+/* Testing only: flags that select an alternative form of a stage with
+ * identical results (the parity tests A/B them), OR-ed into every later call
+ * on ctx; the same bits as pdp_bound_params.reserved.  0 (the default) is the
+ * shipped path.  Timing-ablation flags (results invalid) are refused unless
+ * the library was built with -DPDP_DEBUG_BUILD. */
+int pdp_ctx_set_debug(pdp_ctx* ctx, int32_t flags);
 
 /* Bytes of device workspace pdp_bound_accumulate needs for these columns. */
 int pdp_workspace_size(const pdp_columns* cols, const pdp_bound_params* bp, size_t* bytes);

@@ -49,6 +49,9 @@ constexpr int kThreads = 256;
 #endif
 constexpr int kItems = PDP_OS_ITEMS;         // rows per thread in a radix tile
 constexpr int kTile = kThreads * kItems;     // 4096 rows per radix tile (16 rows per thread)
+// k_histogram_tiles' 16-byte column loads take rows in pairs; the variant builds that pass the GPU suite
+// (16 rows per thread, and 12 in round 4's r04a) are the ones allowed here.
+static_assert(kItems % 2 == 0 && (kItems == 16 || kItems == 12), "tile shape not validated on the GPU");
 // Round 3's 12-rows-per-thread build (3072-row tiles) faulted: the per-tile
 // count loops stepped over the items in groups of kHistUnroll = 8 rows per
 // thread (items 0-7, 8-15) without stopping at kItems = 12, so every tile's
@@ -89,9 +92,6 @@ struct __align__(16) Rec {
 
 #ifndef PDP_OS_NT
 #define PDP_OS_NT 0
-#endif
-#ifndef PDP_DIGIT_MODE6_BRANCH
-#define PDP_DIGIT_MODE6_BRANCH 0
 #endif
 #ifndef PDP_SCATTER_CHECK
 #define PDP_SCATTER_CHECK 0
@@ -237,6 +237,27 @@ constexpr int kDebugForceFilter = 268435456;   // use the L0 pre-filter whenever
 constexpr int kDebugNoThin = 536870912;        // bound the pre-filter's survivors with k_lean instead of k_thin
 constexpr int kDebugFilterTiming = 1073741824;  // k_filter timing ablation: phase 1 only (results invalid)
 constexpr int kDebugLinfSort = 1 << 22;  // lean_segment_sorted: L_inf by a second wave sort (round-2 form)
+// Alternative forms with identical results (parity tests A/B them; pdp_bound_params.reserved or
+// pdp_ctx_set_debug), replacing round 4's PDP_* environment knobs: the shipped library reads no
+// environment and has one semantics ("Determinism").
+constexpr int kDebugNoK4 = 1;               // K4 off: the round-2 fp64-atomic accumulation (last bits differ)
+constexpr int kDebugK4P16 = 2;              // K4 pair passes on 16-byte records even when 12-byte ones fit
+constexpr int kDebugK4Soa = 4;              // K4 12-byte slots written split (keys, then values)
+constexpr int kDebugOddGrid = 8;            // K2 grids of 7 (k_thin) / 5 (k_lean) blocks: determinism tests
+constexpr int kDebugSortTileScan = 16;      // sort_recs by reduce-then-scan instead of decoupled look-back
+constexpr int kDebugAnaNpartAtomics = 32;   // utility analysis: n_partitions by one atomic per pair
+constexpr int kDebugAnaPack = 64;           // utility analysis: separate pack kernel before the sort
+constexpr int kDebugAnaFlags = 128;         // utility analysis: round-3 per-row flags + scan pair extraction
+constexpr int kDebugAnaSelLds = 256;        // utility analysis: round-3 per-regime selection kernels
+constexpr int kDebugK4TileScan = 1024;      // K4 pair passes by reduce-then-scan
+// Timing ablations whose results are invalid: accepted only by a -DPDP_DEBUG_BUILD library.
+constexpr int kAblationFlags = kDebugSortOnly | kDebugNoLookback | kDebugLinearWrite | kDebugNoScatter |
+                               kDebugNoAtomics | kDebugWalkOnly | kDebugNoLinf | kDebugNoSums | kDebugFilterTiming;
+#ifdef PDP_DEBUG_BUILD
+constexpr bool kDebugBuild = true;
+#else
+constexpr bool kDebugBuild = false;
+#endif
 
 struct AccPtrs {
   unsigned long long* row_count;
@@ -257,22 +278,11 @@ __device__ __forceinline__ uint32_t digit_of(const KeySpec& ks, int pass, const 
   const int sh = ks.shift[pass];
   uint64_t key;
   // Mode 6 (K4 pair records) keys like mode 0; its empty slots are dropped by
-  // the caller (onesweep_body).  Round 3 blamed an early-return branch here for
-  // wrong survivor / analysis sort digits; round 4 re-ran the suites with it
-  // (PDP_DIGIT_MODE6_BRANCH=1): green -- the cause was stale look-back status
-  // words (next_epoch), DESIGN.md 3.1c.
-#if PDP_DIGIT_MODE6_BRANCH  // round-3 form, for the miscompile re-check (variant builds only)
-  if (ks.mode == 0) {
-    key = (uint64_t)(r.pid >> ks.low);
-  } else if (ks.mode == 6) {
-    if (r.pid == 0xFFFFFFFFu) return 256u;  // empty slot
-    key = (uint64_t)(r.pid >> ks.low);
-  } else if (ks.mode == 4) {
-#else
+  // the caller (onesweep_body).  (Round 3's "miscompile" of an early-return
+  // branch here was stale look-back status words)
   if (ks.mode == 0 || ks.mode == 6) {
     key = (uint64_t)(r.pid >> ks.low);
   } else if (ks.mode == 4) {
-#endif
     if (sh >= 64) return (uint32_t)(((uint64_t)r.pid * ks.mult) >> 32);
     key = (uint64_t)r.pid;
   } else if (ks.mode == 1) {
@@ -1328,17 +1338,16 @@ __global__ void k_stream_groups(const Rec* __restrict__ r, const long long* __re
 }
 
 // The big kept groups: one block per group.  Each round the block reads 256
-// consecutive rows (coalesced keep bytes), each thread adds its kept row's
-// terms, and a fixed-shape block tree sums the round; round sums are added in
-// row order.  The order depends only on the group's rows, so the result is
-// identical run to run (it is not the sequential input-order sum of
-// k_stream_groups: fp64 sums differ from it in the last bits).
+// consecutive rows (coalesced keep bytes and values) and stages the kept rows'
+// terms in LDS; one thread adds them in row order.  The sum is therefore the
+// sequential input-order sum of k_stream_groups (and of the reference's
+// per-group accumulator), bit for bit (round 4 used a block tree here).
 __global__ __launch_bounds__(kThreads) void k_stream_big_groups(const Rec* __restrict__ r,
                                                                 const long long* __restrict__ gpos,
                                                                 const uint8_t* __restrict__ row_keep, SegParams sp,
                                                                 AccPtrs acc, const unsigned long long* __restrict__ big) {
-  __shared__ double s_x[kThreads / 64], s_y[kThreads / 64];
-  __shared__ unsigned int s_c[kThreads / 64];
+  __shared__ double s_x[kThreads], s_y[kThreads];
+  __shared__ unsigned long long s_m[kThreads / 64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t nbig = (int64_t)big[0];
   for (int64_t b = blockIdx.x; b < nbig; b += gridDim.x) {
@@ -1348,30 +1357,21 @@ __global__ __launch_bounds__(kThreads) void k_stream_big_groups(const Rec* __res
     double x = 0.0, y = 0.0;
     for (long long base = q0; base < q1; base += kThreads) {
       const long long q = base + threadIdx.x;
-      double xt = 0.0, yt = 0.0;
-      unsigned int ct = 0;
-      if (q < q1 && row_keep[q]) {
-        row_terms(sp, r[q].val, xt, yt);
-        ct = 1;
-      }
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) {
-        xt += __shfl_down(xt, o);
-        yt += __shfl_down(yt, o);
-        ct += __shfl_down(ct, o);
-      }
-      if (lane == 0) {
-        s_x[w] = xt;
-        s_y[w] = yt;
-        s_c[w] = ct;
-      }
+      const bool kept = q < q1 && row_keep[q];
+      if (kept) row_terms(sp, r[q].val, s_x[threadIdx.x], s_y[threadIdx.x]);
+      const unsigned long long m = __ballot(kept);
+      if (lane == 0) s_m[w] = m;
       __syncthreads();
       if (threadIdx.x == 0) {
-#pragma unroll
         for (int i = 0; i < kThreads / 64; ++i) {
-          x += s_x[i];
-          y += s_y[i];
-          c += s_c[i];
+          unsigned long long mm = s_m[i];
+          c += (uint32_t)__popcll(mm);
+          while (mm) {
+            const int l = 64 * i + __builtin_ctzll(mm);
+            mm &= mm - 1ull;
+            x += s_x[l];
+            y += s_y[l];
+          }
         }
       }
       __syncthreads();
@@ -1856,6 +1856,7 @@ SegParams make_seg(const pdp_bound_params* bp, int low, int pkb, bool has_value)
 
 struct pdp_ctx {
   int device = 0;
+  int debug = 0;  // pdp_ctx_set_debug: alternative-form flags OR-ed into every call (testing)
   unsigned int tile_slot = kCtrTile0;  // next free onesweep tile-claim counter
   bool prof = false;
   struct ProfRec {
@@ -2042,7 +2043,7 @@ int sort_recs(pdp_ctx* ctx, Rec* a, Rec* b, int64_t m, const KeySpec& ks, unsign
   const int64_t tiles = (m + kTile - 1) / kTile;
   // decoupled look-back passes (no tile-count upsweeps): c3 survivor sort 2.15 -> 2.02 ms, c5 (pk, pid)
   // sort 7.26 -> 6.48 ms (same box); PDP_SORT_TILESCAN=1 restores reduce-then-scan
-  const bool rts = use_tile_scan(m, 0) && env_int("PDP_SORT_TILESCAN", 0) != 0;
+  const bool rts = use_tile_scan(m, 0) && (ctx->debug & kDebugSortTileScan) != 0;
   for (int p = 0; p < ks.passes; ++p) {
     const unsigned int* bases = nullptr;
     // the fused first pass of the utility analysis reads the SoA columns: its tile counts would need
@@ -2073,7 +2074,7 @@ int sort_recs(pdp_ctx* ctx, Rec* a, Rec* b, int64_t m, const KeySpec& ks, unsign
 
 KeySpec composite_spec(int mode, int hi_bits, int lo_bits, int pkb, uint64_t U, uint32_t P) {
   KeySpec ks{};
-  ks.xcd_remap = env_int("PDP_XCD_REMAP", 1);
+  ks.xcd_remap = 1;
   ks.mode = mode;
   ks.low = 0;
   ks.pkb = pkb;
@@ -2263,7 +2264,7 @@ double noise_scale(int kind, double eps, double delta, double l0, double linf) {
   return pdp_gaussian_sigma(eps, delta, std::sqrt(l0) * linf);
 }
 
-bool k4_enabled(int64_t n, bool sweep);
+bool k4_enabled(int64_t n, bool sweep, int debug = 0);
 
 }  // namespace
 
@@ -2384,6 +2385,14 @@ int pdp_sweep_workspace_size(const pdp_columns* cols, size_t* bytes) {
   return 0;
 }
 
+int pdp_ctx_set_debug(pdp_ctx* ctx, int32_t flags) {
+  if (!ctx) return fail(PDP_ERR_INVALID_ARG, "null argument");
+  if ((flags & kAblationFlags) && !kDebugBuild)
+    return fail(PDP_ERR_INVALID_ARG, "timing-ablation debug flags need a -DPDP_DEBUG_BUILD library");
+  ctx->debug = flags;
+  return 0;
+}
+
 int pdp_get_stats(pdp_ctx* ctx, pdp_stats* out) {
   if (!ctx || !out) return fail(PDP_ERR_INVALID_ARG, "null argument");
   *out = ctx->stats;
@@ -2403,7 +2412,10 @@ struct FilterPlan {
   int low_bits;   // pid bits that tell the ids of one bucket apart
 };
 
+// Environment knobs exist only in -DPDP_DEBUG_BUILD libraries (experiment builds,
+// tools/copy_probe.py): the shipped library reads no environment.
 int env_int(const char* name, int def) {
+  if (!kDebugBuild) return def;
   const char* v = std::getenv(name);
   return v && *v ? std::atoi(v) : def;
 }
@@ -2452,17 +2464,18 @@ int k4_exponent(double M) {
   return std::max(-1000, std::min(1000, 62 - e));
 }
 
-bool k4_enabled(int64_t n, bool sweep) { return !sweep && n < (1ll << 32) && env_int("PDP_K4", 1) != 0; }
+bool k4_enabled(int64_t n, bool sweep, int debug) {
+  return !sweep && n < (1ll << 32) && !(debug & kDebugNoK4);
+}
 
 K4Plan k4_plan(const pdp_bound_params* bp, const SegParams& sp, int64_t n, int64_t P, bool sweep) {
   K4Plan k{};
-  k.on = k4_enabled(n, sweep);
+  k.on = k4_enabled(n, sweep, sp.debug);
   if (!k.on) return k;
   const int pkb = std::max(1, pdp::ceil_log2_u64((uint64_t)std::max<int64_t>(P, 1)));
   // the 2048-partition window (56 KiB of LDS: 2 reduce workgroups per CU) unless the 4096 one saves a pass
   auto npasses = [&](int sh) { return (std::max(1, pkb - sh) + 7) / 8; };
   k.sh = npasses(kK4ShMax) < npasses(kK4ShMax - 1) ? kK4ShMax : kK4ShMax - 1;
-  if (const int e = env_int("PDP_K4_SH", 0)) k.sh = std::min(kK4ShMax, std::max(kK4ShMax - 2, e));
   const int kb = std::max(1, pkb - k.sh);
   k.passes = (kb + 7) / 8;
   int rem = kb, sh = 0;
@@ -2487,11 +2500,11 @@ K4Plan k4_plan(const pdp_bound_params* bp, const SegParams& sp, int64_t n, int64
   // the count is used only by COUNT / MEAN / VARIANCE; without it K2 does not sample rows (the slot's count
   // is the group's row count, unbounded), so the key carries no count bits
   k.cb = sp.want_count ? pdp::ceil_log2_u64((uint64_t)std::max(1.0, linf)) : 0;
-  k.p12 = pkb + k.cb <= 31 && env_int("PDP_K4_P12", 1) != 0;
+  k.p12 = pkb + k.cb <= 31 && !(sp.debug & kDebugK4P16);
   // split slots (PDP_K4_SOA=1; parity-green): look-back passes only (k_pair_tile_counts reads 12-byte
   // slots).  Off: c4 pair passes 8.40 / 8.63 ms against 8.35 / 8.34 with 12-byte slots, c3 0.65 against
   // 0.62 (the values wait for their keys), for 1 % fewer pair-pass bytes (r04z7)
-  k.soa = k.p12 && env_int("PDP_K4_SOA", 0) != 0 && env_int("PDP_K4_TILESCAN", 0) == 0;
+  k.soa = k.p12 && (sp.debug & kDebugK4Soa) && !(sp.debug & kDebugK4TileScan);
   return k;
 }
 
@@ -2505,7 +2518,7 @@ K4Red k4_red(const K4Plan& k, const SegParams& sp, int64_t P, bool y) {
   r.q = std::ldexp(1.0, f);
   r.inv_hi = std::ldexp(1.0, 32 - f);
   r.inv_lo = std::ldexp(1.0, -f);
-  r.chunk = std::max(4096, env_int("PDP_K4_CHUNK", (int)kK4Chunk));
+  r.chunk = kK4Chunk;
   r.cb = k.p12 ? k.cb : 0;
   return r;
 }
@@ -2522,7 +2535,7 @@ int k4_run(pdp_ctx* ctx, hipStream_t stream, const K4Plan& k, const K4Red& kr, b
   hipLaunchKernelGGL(k4_set_counter, dim3(1), dim3(64), 0, stream, counters, (int)kCtrK4In,
                      (unsigned long long)total);
   KeySpec ks{};
-  ks.xcd_remap = env_int("PDP_XCD_REMAP", 1);
+  ks.xcd_remap = 1;
   ks.mode = 6;
   ks.cap = std::min<int64_t>(total, buf_cap);  // the pairs (< total) land in buf1 / buf2
   ks.soa_a = soa_a;
@@ -2540,7 +2553,7 @@ int k4_run(pdp_ctx* ctx, hipStream_t stream, const K4Plan& k, const K4Red& kr, b
   // decoupled look-back passes; PDP_K4_TILESCAN=1: reduce-then-scan (tile digit counts, scanned tile
   // bases, tiles in XCD-contiguous runs) -- parity-green, but c4 pair passes 8.31 -> 8.60 ms with it
   // (the counts re-read 8 GB of slots; same box r04i), c3 / c2 unchanged
-  const bool rts = use_tile_scan(total, 0) && env_int("PDP_K4_TILESCAN", 0) != 0;
+  const bool rts = use_tile_scan(total, 0) && (ctx->debug & kDebugK4TileScan) != 0;
   {
     ProfScope ps(ctx, PDP_STAGE_PAIR_PASS, stream);
     for (int p = 0; p < k.passes; ++p) {
@@ -2634,6 +2647,9 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
       return fail(PDP_ERR_INVALID_ARG, "value column required for SUM/MEAN/VARIANCE");
     if (!a->row_count) return fail(PDP_ERR_INVALID_ARG, "row_count accumulator required");
     sps[c] = make_seg(b, plan.low, plan.pkb, cols->value != nullptr);
+    sps[c].debug |= ctx->debug;
+    if ((sps[c].debug & kAblationFlags) && !kDebugBuild)
+      return fail(PDP_ERR_INVALID_ARG, "timing-ablation debug flags need a -DPDP_DEBUG_BUILD library");
     if (sps[c].want_count && !a->count) return fail(PDP_ERR_INVALID_ARG, "count accumulator required");
     if (parts) {
       if (sps[c].xmode != kXNone && (!parts->x_hi || !parts->x_lo || !parts->nan))
@@ -2710,7 +2726,7 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
     ctx->stats.k4_slots = nslots + nkf;
     ctx->stats.k4_passes = k4.passes;
     K4Red krx = k4_red(k4, q, P, false), kry = k4_red(k4, q, P, true);
-    if (!env_int("PDP_K4_CHUNK", 0)) {
+    {
       // records per reduce workgroup: 32768, fewer for small inputs so that the reduction still has
       // about 1024 workgroups (a rank's share of a multi-GPU step: c3 at 8 GPUs has ~8e6 slots)
       const int64_t c = std::min<int64_t>(kK4Chunk, std::max<int64_t>(4096, (nslots + nkf) / 1024 / 4096 * 4096));
@@ -2759,7 +2775,7 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
 
   sp.packed = !k4.on && sp.want_count && n < (1ll << 32);
   KeySpec ks{};
-  ks.xcd_remap = env_int("PDP_XCD_REMAP", 1);
+  ks.xcd_remap = 1;
   ks.mode = 0;
   ks.low = plan.low;
   ks.pkb = plan.pkb;
@@ -2809,7 +2825,7 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
   // decoupled look-back against 2 x 3.22 ms + 1.06 ms per pass of tile counts with the XCD-contiguous
   // tile runs (step 38.31 -> 37.81 ms, same box r04h; round 3, before the loads-ahead passes, had
   // measured the reverse).  PDP_PASS_TILESCAN=0: look-back.
-  const bool rest_tile_scan = env_int("PDP_PASS_TILESCAN", 1) != 0;
+  const bool rest_tile_scan = true;
   for (int p = 0; p < ks.passes; ++p) {
     const unsigned int* bases = nullptr;
     if (rts && (p == 0 || rest_tile_scan)) {
@@ -2921,9 +2937,9 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
       const int64_t waves = ((int64_t)n_sorted + kThinChunk - 1) / kThinChunk;
       // LDS partition cache on: the Zipf-head pairs' HBM atomics otherwise dominate (c3: K2 8.1 -> 3.4 ms);
       // K4 writes pair records instead of atomics, no cache
-      const bool tcache = !k4.on && env_int("PDP_THIN_CACHE", 1) != 0;
+      const bool tcache = !k4.on;
       const int64_t blocks =
-          std::max<int64_t>(1, std::min<int64_t>((waves + 3) / 4, env_int("PDP_THIN_BLOCKS", 8192)));
+          std::max<int64_t>(1, std::min<int64_t>((waves + 3) / 4, (sp.debug & kDebugOddGrid) ? 7 : 8192));
       const int64_t l0 = bp->max_partitions_contributed;
       auto kern = l0 <= 1 ? (tcache ? k_thin<true, 1> : k_thin<false, 1>)
                 : l0 <= 2 ? (tcache ? k_thin<true, 2> : k_thin<false, 2>)
@@ -2934,14 +2950,14 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
     } else if (bp->max_partitions_contributed <= kLeanMaxL0 && !(sp.debug & kDebugBatchKernel)) {
       const int64_t waves = ((int64_t)n_sorted + kLeanChunk - 1) / kLeanChunk;
       int64_t max_blocks = (sp.debug & kDebugFewBlocks) ? 4096 : kLeanMaxBlocks;
-      if (fpl.on) max_blocks = env_int("PDP_K2_BLOCKS", (int)max_blocks);
+      if (sp.debug & kDebugOddGrid) max_blocks = 5;
       const int64_t blocks = std::max<int64_t>(1, (waves + 3) / 4 < max_blocks ? (waves + 3) / 4 : max_blocks);
       const bool sorted_l0 = bp->max_partitions_contributed >= kSortMinL0 && !(sp.debug & kDebugLeanMinSearch);
       // the LDS partition cache pays when many privacy ids keep the same hot partitions, which grows with
       // L0: c4 (L0 = 32) K2 137 -> 50 ms (round 1); at c3 (L0 = 4) / c2 (L0 = 8) it does not pay
       const bool cache = !k4.on &&
                          (bp->max_partitions_contributed >= kHotMinL0 || (sp.debug & kDebugForceHotCache) ||
-                          (fpl.on && env_int("PDP_K2_CACHE", 0))) &&
+                          false) &&
                          !(sp.debug & kDebugNoHotCache);
       const bool two = bp->max_partitions_contributed > 64;
       auto kern = sorted_l0 ? (two ? (cache ? k_lean<2, true, true> : k_lean<2, true, false>)
@@ -3238,14 +3254,14 @@ int analysis_impl(pdp_ctx* ctx, const int64_t* pid, const int64_t* pk, const dou
                                   (uint32_t)P);
       // round 4: the packing is fused into the histogram and the first pass (c5: -0.94 ms of k_ana_pack,
       // +8 B per row in the first pass); PDP_ANA_PACK=1 restores the separate pack
-      const bool fused = ks.passes > 0 && !env_int("PDP_ANA_PACK", 0);
+      const bool fused = ks.passes > 0 && !(ctx->debug & kDebugAnaPack);
       if (!fused)
         hipLaunchKernelGGL(k_ana_pack, dim3(g), dim3(kThreads), 0, stream, pid, pk, val, n, U, P, ra, counters);
       if (int rc = sort_recs(ctx, ra, rb, n, ks, hist, off, counters, status, status_bytes, workspace, stream, &sorted,
                              PDP_STAGE_ANALYSIS_SORT, fused ? pid : nullptr, fused ? pk : nullptr,
                              fused ? val : nullptr))
         return rc;
-      if (env_int("PDP_ANA_FLAGS", 0)) {  // round-3 form: per-row flags, scan, one thread per group start
+      if (ctx->debug & kDebugAnaFlags) {  // round-3 form: per-row flags, scan, one thread per group start
         hipLaunchKernelGGL(k_ana_group_flags, dim3(g), dim3(kThreads), 0, stream, sorted, n, flags);
         if (int rc = scan_inplace(flags, n, stream)) return rc;
         hipLaunchKernelGGL(k_ana_pairs, dim3(g), dim3(kThreads), 0, stream, sorted, n, flags, num_sampled, ppk, pref,
@@ -3257,7 +3273,7 @@ int analysis_impl(pdp_ctx* ctx, const int64_t* pid, const int64_t* pk, const dou
         if (int rc = scan_inplace(flags, tiles, stream)) return rc;
         // n_partitions of the sampled pairs: bucketed LDS histogram (np_hist) or one atomic per pair
         np_sh = std::max(0, pidbits - 8);
-        np_hist = np_sh <= 14 && env_int("PDP_ANA_NPART_HIST", 1);
+        np_hist = np_sh <= 14 && !(ctx->debug & kDebugAnaNpartAtomics);
         np_spare = (uint32_t*)(sorted == ra ? rb : ra);
         hipLaunchKernelGGL(k_ana_tile_pairs, dim3((unsigned)tiles), dim3(256), 0, stream, sorted, n, flags, num_sampled,
                            ppk, pref, pcnt, psum, npart, counters, (int)!np_hist);
@@ -3266,7 +3282,7 @@ int analysis_impl(pdp_ctx* ctx, const int64_t* pid, const int64_t* pk, const dou
       // pre-aggregated pairs -> sorted by pk
       hipLaunchKernelGGL(k_ana_pack_pre, dim3(g), dim3(kThreads), 0, stream, pk, val, n, P, ra, counters);
       KeySpec ks{};
-      ks.xcd_remap = env_int("PDP_XCD_REMAP", 1);
+      ks.xcd_remap = 1;
       ks.mode = 0;
       ks.num_pids = 0xFFFFFFFFu;
       ks.num_parts = (uint32_t)P;
@@ -3354,7 +3370,7 @@ int analysis_impl(pdp_ctx* ctx, const int64_t* pid, const int64_t* pk, const dou
   if (priv) {
     ProfScope ps_sel(ctx, PDP_STAGE_ANALYSIS_SELECT, stream);
     const int64_t blocks = std::min<int64_t>((P + kAnaSelWaves - 1) / kAnaSelWaves, 16384);
-    if (L.groups.G > 0 && !env_int("PDP_ANA_SEL_LDS", 0)) {
+    if (L.groups.G > 0 && !(ctx->debug & kDebugAnaSelLds)) {
       hipLaunchKernelGGL(k_ana_select_grouped, dim3((unsigned)std::min<int64_t>(P, 65536), cgroups), dim3(64), 0,
                          stream, pref, npart, pbeg, P, cfg_d, nconf, L.groups, (const double*)mom, out->prob_keep);
     } else {  // round-3 form: one launch per regime, lanes = configurations

@@ -367,6 +367,11 @@ class HipExecutor:
                                              self.stream_handle), "pdp_shard_rows")
         return opid, opk, oval, list(counts)
 
+    def set_debug(self, flags: int = 0):
+        """pdp_ctx_set_debug (testing): alternative-form flags for every later
+        call on this executor (DEBUG_* in native.py); 0 = the shipped path."""
+        native.check(self.lib.pdp_ctx_set_debug(self.ctx, int(flags)), "pdp_ctx_set_debug")
+
     def profile(self, enable: bool = True):
         native.check(self.lib.pdp_profile_enable(self.ctx, int(enable)), "pdp_profile_enable")
 

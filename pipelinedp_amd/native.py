@@ -18,6 +18,19 @@ SELECTION_NONE, SELECTION_TRUNCATED_GEOMETRIC, SELECTION_LAPLACE, SELECTION_GAUS
 MECH_COUNT, MECH_SUM, MECH_MEAN, MECH_VARIANCE, MECH_PRIVACY_ID_COUNT, MECH_SELECTION = range(6)
 NUM_MECH = 6
 
+# Debug flags (pdp_bound_params.reserved / pdp_ctx_set_debug; testing only): alternative forms of a
+# stage with identical results, and the forced-path switches of the parity suite.
+DEBUG_NO_K4 = 1  # round-2 fp64-atomic accumulation instead of K4 (last bits of sums differ)
+DEBUG_K4_P16 = 2
+DEBUG_K4_SOA = 4
+DEBUG_ODD_GRID = 8
+DEBUG_SORT_TILESCAN = 16
+DEBUG_ANA_NPART_ATOMICS = 32
+DEBUG_ANA_PACK = 64
+DEBUG_ANA_FLAGS = 128
+DEBUG_ANA_SEL_LDS = 256
+DEBUG_K4_TILESCAN = 1024
+
 c_i32, c_i64, c_u64, c_f64 = ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64, ctypes.c_double
 c_vp = ctypes.c_void_p
 
@@ -96,6 +109,7 @@ SIGNATURES = [
     ("pdp_last_error", ctypes.c_char_p, []),
     ("pdp_ctx_create", c_vp, [c_i32]),
     ("pdp_ctx_destroy", None, [c_vp]),
+    ("pdp_ctx_set_debug", c_i32, [c_vp, c_i32]),
     ("pdp_workspace_size", c_i32, [ctypes.POINTER(Columns), ctypes.POINTER(BoundParams),
                                    ctypes.POINTER(ctypes.c_size_t)]),
     ("pdp_bound_accumulate", c_i32, [c_vp, ctypes.POINTER(Columns), ctypes.POINTER(BoundParams),

@@ -217,9 +217,9 @@ def test_analysis_after_aggregate_on_one_workspace(ex):
     np.testing.assert_array_equal(p1.cpu().numpy(), p2.cpu().numpy())
 
 
-def test_analysis_sort_forms_bitwise_equal(ex, monkeypatch):
+def test_analysis_sort_forms_bitwise_equal(ex):
     """The (pk, pid) sort by decoupled look-back (default) and reduce-then-scan
-    (PDP_SORT_TILESCAN=1; its fused first pass still runs by look-back) give
+    (debug flag SORT_TILESCAN; its fused first pass still runs by look-back) give
     the same per-partition metrics bit for bit.  A round-4 build took the
     reduce-then-scan tile counts of the fused first pass from the unwritten
     record buffer."""
@@ -232,19 +232,23 @@ def test_analysis_sort_forms_bitwise_equal(ex, monkeypatch):
     mask = native.METRIC_SUM | native.METRIC_COUNT | native.METRIC_PRIVACY_ID_COUNT
     d = lambda a: torch.from_numpy(a).cuda()  # noqa: E731
     runs = []
-    for form in ("0", "1"):
-        monkeypatch.setenv("PDP_SORT_TILESCAN", form)
-        m, prob, _ = ex.analyze(d(pid), d(pk), d(val), U, P, mask, cfgs)
-        torch.cuda.synchronize()
+    for form in (0, native.DEBUG_SORT_TILESCAN):
+        ex.set_debug(form)
+        try:
+            m, prob, _ = ex.analyze(d(pid), d(pk), d(val), U, P, mask, cfgs)
+            torch.cuda.synchronize()
+        finally:
+            ex.set_debug(0)
         runs.append((m.cpu().numpy(), prob.cpu().numpy()))
     np.testing.assert_array_equal(runs[0][0], runs[1][0])
     np.testing.assert_array_equal(runs[0][1], runs[1][1])
 
 
-def test_analysis_npart_forms_bitwise_equal(ex, monkeypatch):
+def test_analysis_npart_forms_bitwise_equal(ex):
     """n_partitions per privacy id from one atomic per pair (default) or from the bucketed LDS
-    histogram of the sampled pairs' ids (PDP_ANA_NPART_HIST=1; the pairs of partitions that are
-    not sampled keep their atomics): identical metrics, keep probabilities and exported pairs,
+    histogram of the sampled pairs' ids (default; the pairs of partitions that are
+    not sampled keep their atomics; debug flag ANA_NPART_ATOMICS forces the atomics): identical
+    metrics, keep probabilities and exported pairs,
     with all partitions sampled and with a third of them."""
     import torch
     from pipelinedp_amd import native
@@ -256,11 +260,14 @@ def test_analysis_npart_forms_bitwise_equal(ex, monkeypatch):
     d = lambda a: torch.from_numpy(a).cuda()  # noqa: E731
     for ns in (None, P // 3):
         runs = []
-        for form in ("0", "1"):
-            monkeypatch.setenv("PDP_ANA_NPART_HIST", form)
-            m, prob, ids = ex.analyze(d(pid), d(pk), d(val), U, P, mask, cfgs, num_sampled_partitions=ns)
-            pairs = ex.preaggregate(d(pid), d(pk), d(val), U, P, num_sampled_partitions=ns)
-            torch.cuda.synchronize()
+        for form in (native.DEBUG_ANA_NPART_ATOMICS, 0):
+            ex.set_debug(form)
+            try:
+                m, prob, ids = ex.analyze(d(pid), d(pk), d(val), U, P, mask, cfgs, num_sampled_partitions=ns)
+                pairs = ex.preaggregate(d(pid), d(pk), d(val), U, P, num_sampled_partitions=ns)
+                torch.cuda.synchronize()
+            finally:
+                ex.set_debug(0)
             runs.append([m.cpu().numpy(), prob.cpu().numpy(), ids.cpu().numpy()] +
                         [t.cpu().numpy() for t in pairs])
         for a, b in zip(runs[0], runs[1]):

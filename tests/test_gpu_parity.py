@@ -1,9 +1,15 @@
 """GPU parity: the HIP path (through the C ABI) against the CPU oracle and the
 reference golden vectors.
 
-Tolerances: counts / privacy-id counts / keep decisions bit-exact; fp64 sums
-|gpu - oracle| <= 1e-9 * (sum of |terms| + 1) (summation order differs);
-noisy outputs with identical Philox draws rel 1e-9 (libm ulps).
+Tolerances: counts / privacy-id counts / keep decisions bit-exact.  fp64
+sums bit-exact too (check_acc with the bounds): every K2 kernel and the
+generic path sum a (pid, pk) group's kept rows in input order, as the oracle
+does (np.bincount over the stably sorted rows) and as the reference's
+per-group create_accumulator does (combiners.py:305-311, 364-373), and K4 adds
+the pairs' rint(x 2^F) exactly, so GPU x / y == o.k4_finalize(o.k4_partials(
+...)) bit for bit.  (Tolerance |d| <= 1e-9 (sum |terms| + 1) remains only for
+the fp64-atomic forms: NO_K4 and the parameter sweep.)
+Noisy outputs with identical Philox draws rel 1e-9 (libm ulps).
 """
 import math
 
@@ -29,6 +35,7 @@ def _dev(a, torch):
 
 
 BATCH_KERNEL = 4096  # debug flag: k_segments (register bitonic batches) instead of k_lean
+NO_K4, K4_P16, K4_SOA, ODD_GRID = 1, 2, 4, 8  # debug flags (native.DEBUG_*): alternative forms
 
 
 def run_gpu(ex, pid, pk, val, U, P, bp: o.BoundParams, mask, seed=3, fallback=False, debug_flags=0):
@@ -43,10 +50,17 @@ def run_gpu(ex, pid, pk, val, U, P, bp: o.BoundParams, mask, seed=3, fallback=Fa
     return cfg, acc, g(acc.row_count), g(acc.count), g(acc.x), g(acc.y)
 
 
-def check_acc(ref, rc, cnt, x, y, mask, value=None):
+def check_acc(ref, rc, cnt, x, y, mask, value=None, bp=None):
     np.testing.assert_array_equal(rc, ref.row_count)
     if cnt is not None:
         np.testing.assert_array_equal(cnt, ref.count)
+    if bp is not None:
+        # input-order pair sums + exact fixed-point merge: bit for bit (module docstring)
+        kx, ky = o.k4_finalize(o.k4_partials(ref, len(rc), bp, mask), bp, mask)
+        if x is not None and kx is not None:
+            np.testing.assert_array_equal(x, kx)
+        if y is not None and ky is not None:
+            np.testing.assert_array_equal(y, ky)
     scale = 1e-9 * ((ref.count + 1) * (1.0 if value is None else max(1.0, float(np.abs(value).max())))**2) + 1e-9
     if mask & (4 | 8):
         assert np.all(np.abs(x - ref.nsum) <= scale)
@@ -105,7 +119,7 @@ def test_bound_accumulate_matches_oracle(ex, cfgi, mode):
                                                "filter_lean": FORCE_FILTER | NO_THIN,
                                                "filter_batch": FORCE_FILTER | BATCH_KERNEL}.get(mode, 0))
     ref = o.bound_and_accumulate(pid, pk, val if need_val else None, P, bp, "hash", seed=77 + cfgi)
-    check_acc(ref, rc, cnt, x, y, mask, val)
+    check_acc(ref, rc, cnt, x, y, mask, val, bp)
     st = ex.stats()
     if cfgi == 5 and "fallback" not in mode:
         assert st.fallback_rows > 0  # huge privacy ids went through the generic path
@@ -138,7 +152,7 @@ def test_prefilter_matches_unfiltered_at_scale(ex, L0, Linf, z, rows_per_pid):
     np.testing.assert_array_equal(cnt, cnt2)
     np.testing.assert_allclose(x, x2, rtol=1e-9, atol=1e-9)
     ref = o.bound_and_accumulate(pid, pk, val, P, bp, "hash", seed=9)
-    check_acc(ref, rc, cnt, x, None, mask, val)
+    check_acc(ref, rc, cnt, x, None, mask, val, bp)
 
 
 def test_full_width_privacy_ids_and_wide_partition_ids(ex):
@@ -156,7 +170,7 @@ def test_full_width_privacy_ids_and_wide_partition_ids(ex):
     for fallback in (False, True):
         _, _, rc, cnt, x, _ = run_gpu(ex, pid, pk, val, U, P, bp, 1 | 4 | 16, seed=31, fallback=fallback)
         ref = o.bound_and_accumulate(pid, pk, val, P, bp, "hash", seed=31)
-        check_acc(ref, rc, cnt, x, None, 1 | 4 | 16, val)
+        check_acc(ref, rc, cnt, x, None, 1 | 4 | 16, val, bp)
     assert ex.stats().sort_passes == 4
 
 
@@ -180,7 +194,7 @@ def test_prefilter_half_sketch_wide_buckets(ex, L0, Linf):
     assert surv == int(o.prefilter_survivors(pid, pk, 21, L0, 16).sum())
     assert surv < n
     ref = o.bound_and_accumulate(pid, pk, val, P, bp, "hash", seed=21)
-    check_acc(ref, rc, cnt, x, None, mask, val)
+    check_acc(ref, rc, cnt, x, None, mask, val, bp)
 
 
 @pytest.mark.parametrize("flags", [0, FORCE_FILTER])
@@ -193,7 +207,7 @@ def test_dropped_rows_and_public_partitions(ex, flags):
     assert ex.stats().kept_rows_in == int((pk >= 0).sum())
     assert (ex.stats().filter_rows > 0) == bool(flags)
     ref = o.bound_and_accumulate(pid, pk, val, P, bp, "hash", seed=3)
-    check_acc(ref, rc, cnt, x, None, 1 | 2 | 16, val)
+    check_acc(ref, rc, cnt, x, None, 1 | 2 | 16, val, bp)
     assert rc[::3].sum() == 0
     pk_all = np.full(n, -1)
     _, _, rc, cnt, x, _ = run_gpu(ex, pid, pk_all, val, U, P, bp, 1 | 2, debug_flags=flags)
@@ -227,20 +241,7 @@ def test_already_enforced_matches_oracle(ex):
     bp = o.BoundParams(3, 2, 0.0, 10.0, contribution_bounds_already_enforced=True)
     _, _, rc, cnt, x, _ = run_gpu(ex, None, pk, val, 1, P, bp, 1 | 2)
     ref = o.bound_and_accumulate(None, pk, val, P, bp)
-    check_acc(ref, rc, cnt, x, None, 1 | 2, val)
-
-
-def _with_env(name, value, fn):
-    import os
-    old = os.environ.get(name)
-    os.environ[name] = value
-    try:
-        return fn()
-    finally:
-        if old is None:
-            del os.environ[name]
-        else:
-            os.environ[name] = old
+    check_acc(ref, rc, cnt, x, None, 1 | 2, val, bp)
 
 
 @pytest.mark.parametrize("flags", [0, FORCE_FILTER, NO_THIN | FORCE_FILTER, BATCH_KERNEL])
@@ -254,25 +255,24 @@ def test_determinism_of_counts_and_sums(ex, flags):
     mask = 1 | 4 | 8 | 16
     r1 = run_gpu(ex, pid, pk, val, U, P, bp, mask, seed=5, debug_flags=flags)
     r2 = run_gpu(ex, pid, pk, val, U, P, bp, mask, seed=5, debug_flags=flags)
-    r3 = _with_env("PDP_THIN_BLOCKS", "7", lambda: _with_env(
-        "PDP_K2_BLOCKS", "5", lambda: run_gpu(ex, pid, pk, val, U, P, bp, mask, seed=5, debug_flags=flags)))
+    r3 = run_gpu(ex, pid, pk, val, U, P, bp, mask, seed=5, debug_flags=flags | ODD_GRID)
     for r in (r2, r3):
         for i in (2, 3, 4, 5):
             np.testing.assert_array_equal(r1[i], r[i])
     ref = o.bound_and_accumulate(pid, pk, val, P, bp, "hash", seed=5)
-    check_acc(ref, r1[2], r1[3], r1[4], r1[5], mask, val)
+    check_acc(ref, r1[2], r1[3], r1[4], r1[5], mask, val, bp)
 
 
 @pytest.mark.parametrize("cfgi", [0, 2, 3, 5, 9, 11, 16, 20])
 def test_k4_reduction_matches_atomic_path(ex, cfgi):
     """The K4 pair-record reduction against the round-2 fp64-atomic
-    accumulation (PDP_K4=0) on the same bounding: counts bit-exact, sums to
+    accumulation (debug flag NO_K4) on the same bounding: counts bit-exact, sums to
     1e-12 relative (only the summation differs)."""
     n, U, P, z, L0, Linf, vb, pb, mask = CONFIGS[cfgi]
     pid, pk, val = o.synth_rows(n, U, P, seed=100 + cfgi, zipf_s=z, value_lo=-5, value_hi=15)
     bp = o.BoundParams(L0, Linf, *(vb or (None, None)), *(pb or (None, None)))
     a = run_gpu(ex, pid, pk, val, U, P, bp, mask, seed=7)
-    b = _with_env("PDP_K4", "0", lambda: run_gpu(ex, pid, pk, val, U, P, bp, mask, seed=7))
+    b = run_gpu(ex, pid, pk, val, U, P, bp, mask, seed=7, debug_flags=NO_K4)
     np.testing.assert_array_equal(a[2], b[2])
     if a[3] is not None:
         np.testing.assert_array_equal(a[3], b[3])
@@ -385,6 +385,32 @@ def test_engine_matches_reference_golden(name, fallback):
             else:
                 n = max(getattr(t, "count", 1.0), 1.0) if "count" in fields else 1000.0
                 assert abs(g - e) <= 1e-9 * (n + 1) * max(vmax, 1.0)**2 + 1e-9, (k, f, g, e)
+
+
+@pytest.mark.parametrize("fallback", [False, True])
+@pytest.mark.parametrize("name", aggregate_cases())
+def test_golden_inputs_accumulate_bitwise_vs_oracle(ex, name, fallback):
+    """The golden cases' own inputs through pdp_bound_accumulate: counts and
+    sums bit for bit against the oracle's accumulators merged in K4's fixed
+    point (the oracle itself equals the reference's LocalBackend on these
+    cases, tests/test_oracle.py; module docstring for the L_inf rule)."""
+    d = load(name)
+    cfg = d["meta"]["cfg"]
+    pid, pk, keys = encode_case(d)
+    enforced = cfg.get("already_enforced", False)
+    bp = o.BoundParams(cfg["L0"], cfg["Linf"], cfg.get("min_value"), cfg.get("max_value"),
+                       cfg.get("min_sum_per_partition"), cfg.get("max_sum_per_partition"), enforced)
+    mask = 0
+    for m in cfg["metrics"]:
+        mask |= MASK[m]
+    has_val = len(d["value"]) > 0
+    val = d["value"].astype(np.float64) if has_val and mask & (2 | 4 | 8) else None
+    P = max(len(keys), 1)
+    U = int(pid.max()) + 1 if len(pid) else 1
+    _, _, rc, cnt, x, y = run_gpu(ex, None if enforced else pid, pk, val, U, P, bp, mask, seed=19,
+                                  fallback=fallback and not enforced)
+    ref = o.bound_and_accumulate(None if enforced else pid, pk, val, P, bp, "hash", seed=19)
+    check_acc(ref, rc, cnt, x, y, mask, val, bp)
 
 
 def test_engine_columnar_device_input_and_select_partitions():
@@ -585,27 +611,26 @@ def test_heavy_single_group_generic_path(ex):
         dt = time.perf_counter() - t0
         assert ex.stats().fallback_rows >= heavy
         ref = o.bound_and_accumulate(pid, pk, val, P, bp, "hash", seed=5)
-        check_acc(ref, rc, cnt, x, y, mask, val)
+        check_acc(ref, rc, cnt, x, y, mask, val, bp)
         assert dt < 0.5, dt
 
 
 @pytest.mark.parametrize("cfgi", [0, 2, 9, 11, 19, 21])
-def test_k4_pair_record_forms_bitwise_equal(ex, cfgi, monkeypatch):
+def test_k4_pair_record_forms_bitwise_equal(ex, cfgi):
     """K4's pair passes move 12-byte records {pk << cb | count - 1, x} when the
     partition id and count fit 31 bits, 16-byte {pk, count, x} otherwise
-    (PDP_K4_P12=0 forces them); K2 writes the 12-byte form as split slots (keys,
-    then values: the first pass reads 4 bytes of an empty slot) unless
-    PDP_K4_SOA=0: the fixed-point sums are integers, so all three forms give
+    (debug flag K4_P16 forces them); K2 can write the 12-byte form as split slots
+    (keys, then values: the first pass reads 4 bytes of an empty slot; flag
+    K4_SOA): the fixed-point sums are integers, so all three forms give
     identical accumulators, sums included."""
     n, U, P, z, L0, Linf, vb, pb, mask = CONFIGS[cfgi]
     pid, pk, val = o.synth_rows(n, U, P, seed=700 + cfgi, zipf_s=z, value_lo=-5, value_hi=15)
     bp = o.BoundParams(L0, Linf, *(vb or (None, None)), *(pb or (None, None)))
     need_val = bool(mask & (2 | 4 | 8))
     runs = []
-    for p12, soa in (("1", "1"), ("1", "0"), ("0", "1")):
-        monkeypatch.setenv("PDP_K4_P12", p12)
-        monkeypatch.setenv("PDP_K4_SOA", soa)
-        _, _, rc, cnt, x, y = run_gpu(ex, pid, pk, val if need_val else None, U, P, bp, mask, seed=5 + cfgi)
+    for form in (K4_SOA, 0, K4_P16 | K4_SOA):
+        _, _, rc, cnt, x, y = run_gpu(ex, pid, pk, val if need_val else None, U, P, bp, mask, seed=5 + cfgi,
+                                      debug_flags=form)
         runs.append((rc, cnt, x, y))
     for other in runs[1:]:
         for a, b in zip(runs[0], other):
@@ -615,9 +640,9 @@ def test_k4_pair_record_forms_bitwise_equal(ex, cfgi, monkeypatch):
                 np.testing.assert_array_equal(a, b)
 
 
-@pytest.mark.parametrize("p12", ["1", "0"])
+@pytest.mark.parametrize("p12", [True, False])
 @pytest.mark.parametrize("cfgi", [0, 5, 9, 11, 17, 19, 21])
-def test_row_counts_only_match_oracle(ex, cfgi, p12, monkeypatch):
+def test_row_counts_only_match_oracle(ex, cfgi, p12):
     """Selection only (no COUNT / SUM: select_partitions' accumulate): K2 does
     not sample rows then, so a pair slot's count is the group's row count, not
     bounded by L_inf; the 12-byte K4 key must not carry count bits (a round-4
@@ -625,8 +650,7 @@ def test_row_counts_only_match_oracle(ex, cfgi, p12, monkeypatch):
     oracle in both record forms."""
     n, U, P, z, L0, Linf, vb, pb, _ = CONFIGS[cfgi]
     pid, pk, _ = o.synth_rows(n, U, P, seed=900 + cfgi, zipf_s=z, value_lo=0, value_hi=1)
-    monkeypatch.setenv("PDP_K4_P12", p12)
     bp = o.BoundParams(L0, Linf)
-    _, _, rc, cnt, x, y = run_gpu(ex, pid, pk, None, U, P, bp, 0, seed=11 + cfgi)
+    _, _, rc, cnt, x, y = run_gpu(ex, pid, pk, None, U, P, bp, 0, seed=11 + cfgi, debug_flags=0 if p12 else K4_P16)
     ref = o.bound_and_accumulate(pid, pk, None, P, bp, "hash", seed=11 + cfgi)
     np.testing.assert_array_equal(rc, ref.row_count)

@@ -112,7 +112,8 @@ def test_dp_engine_with_world_on_rccl_matches_single_process(rccl):
 
 
 @pytest.mark.parametrize("world_size", [2, 3, 8])
-@pytest.mark.parametrize("metrics", ["mean_var", "sum_clip", "sum_partition_bounds"])
+@pytest.mark.parametrize("metrics", ["mean_var", "sum_clip", "sum_partition_bounds", "enforced", "count_only",
+                                     "pid_count_only"])
 def test_partials_over_emulated_ranks_equal_one_gpu_bitwise(world_size, metrics):
     """The multi-GPU merge without a process group: the rows are split by
     shard_of(pid) into world_size shards, each shard runs
@@ -122,7 +123,9 @@ def test_partials_over_emulated_ranks_equal_one_gpu_bitwise(world_size, metrics)
     pdp_bound_accumulate over all rows bit for bit (K4's fixed point is an
     integer sum), for MEAN + VARIANCE (x and y runs), clipped SUM and SUM with
     per-partition sum bounds; a NaN value makes its partition's sums NaN on
-    both paths."""
+    both paths.  Also contribution_bounds_already_enforced (k_enforced -> K4
+    with L_inf = 1) and the COUNT-only / PRIVACY_ID_COUNT-only masks, whose
+    partials carry no x / nan rows (Partials.fields_for)."""
     import torch
     from pipelinedp_amd import native
     from pipelinedp_amd.distributed import shard_of
@@ -139,8 +142,17 @@ def test_partials_over_emulated_ranks_equal_one_gpu_bitwise(world_size, metrics)
                           0.0, 10.0, sampling_seed=12)
     elif metrics == "sum_clip":
         cfg = BoundConfig(M.METRIC_COUNT | M.METRIC_SUM, 4, 3, -2.0, 12.0, sampling_seed=12)
-    else:
+    elif metrics == "sum_partition_bounds":
         cfg = BoundConfig(M.METRIC_SUM, 5, 2, None, None, -3.0, 25.0, sampling_seed=12)
+    elif metrics == "enforced":
+        cfg = BoundConfig(M.METRIC_COUNT | M.METRIC_SUM | M.METRIC_MEAN, 3, 2, 0.0, 10.0,
+                          bounds_already_enforced=True, sampling_seed=12)
+    elif metrics == "count_only":
+        cfg = BoundConfig(M.METRIC_COUNT, 3, 2, sampling_seed=12)
+    else:
+        cfg = BoundConfig(M.METRIC_PRIVACY_ID_COUNT, 2, 1, sampling_seed=12)
+    if metrics in ("count_only", "pid_count_only"):
+        assert "x_hi" not in Partials.fields_for(cfg.metrics_mask)
     d = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
     one = ex.accumulate(d(pid), d(pk), d(val), U, P, cfg)
     shard = shard_of(pid, world_size)
