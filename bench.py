@@ -386,18 +386,28 @@ def main():
     rel = ReleaseConfig(mask, native.NOISE_LAPLACE, selection, eps, delta, 1, True, noise_seed=args.seed + 2)
     fields = native.metric_fields(mask)
 
+    # Stream-ordered steps: the accumulate enqueues without waiting for the stream (PDP_BOUND_ASYNC; its
+    # status is checked once the timed loop has drained), so consecutive steps run back to back on the GPU
+    # and the host enqueues the next step while the current one runs.  Per-step times: hipEvents.
     def step():
         if sweep:
             metrics, prob, pids = ex.analyze(pid, pk, val, U, P, mask, ana_cfgs)
             return (pids > 0,)
         if world is not None:
-            return world.aggregate(ex, pid, pk, val, U, P, bounds, rel, gather=False)
-        acc = ex.accumulate(pid, pk, val, U, P, bounds)
+            return world.aggregate(ex, pid, pk, val, U, P, bounds, rel, gather=False, sync=False)
+        acc = ex.accumulate(pid, pk, val, U, P, bounds, sync=False)
         return ex.release(acc, rel, bounds)
+
+    def check_status():
+        if not sweep:
+            st_code = ex.status()
+            if st_code:
+                raise RuntimeError(f"accumulate status {st_code}: {native.lib().pdp_last_error().decode()}")
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
+    check_status()
     st = ex.stats()
     rows_after_public_filter = int(st.kept_rows_in)
     surv = int(st.filter_rows)  # rows that survive the L0 pre-filter (0: it did not run)
@@ -410,14 +420,16 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    marks = []
-    for _ in range(args.steps):
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
+    ev[0].record()
+    for i in range(args.steps):
         res = step()
-        torch.cuda.synchronize()  # per-step stamps for the median (the path syncs inside each step anyway)
-        marks.append(time.perf_counter())
+        ev[i + 1].record()  # per-step stamps for the median (no host wait inside the timed loop)
+    torch.cuda.synchronize()
     if world is not None:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    check_status()
     if world is not None:
         t = torch.tensor([elapsed], device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -488,7 +500,7 @@ def main():
         del acc
 
     rows_per_s = n * world_size * args.steps / elapsed
-    step_s = sorted(b - a for a, b in zip([t0] + marks[:-1], marks))
+    step_s = sorted(ev[i].elapsed_time(ev[i + 1]) * 1e-3 for i in range(args.steps))
     med = step_s[len(step_s) // 2] if len(step_s) % 2 else 0.5 * (step_s[len(step_s) // 2 - 1] + step_s[len(step_s) // 2])
     copy_gbs = copy_peak_gbs(torch, native.lib()) if rank == 0 and not args.no_profile else None
     if roofline is not None:
@@ -508,7 +520,9 @@ def main():
             "value": rows_per_s, "unit": "rows/s", "n_gpus": world_size, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
             "ms_per_step_median": med * 1e3, "value_median_step": n * world_size / med,
-            "median_note": "median of the per-step times on rank 0 (BASELINE.md: median); value = K steps / total",
+            "median_note": "median of the per-step hipEvent times on rank 0 (BASELINE.md: median); value = K steps / "
+                           "total wall time between the synchronised brackets",
+            "host_waits_per_step": int(ex.stats().host_waits) if not sweep else None,
             "scaling": "strong" if args.strong else "weak", "vs_baseline": None, "dtype": "f64",
             "data": "synthetic (on-device Philox generator, oracle/pdp_oracle.py:synth_rows)",
             "config": {"workload": (f"c5: UtilityAnalysisEngine.analyze, {len(SWEEP)} configurations "

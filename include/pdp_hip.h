@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define PDP_ABI_VERSION 1
+#define PDP_ABI_VERSION 2
 
 enum {
   PDP_OK = 0,
@@ -50,6 +50,17 @@ enum {
   PDP_ERR_WORKSPACE = -3,
   PDP_ERR_OUT_OF_RANGE = -4,
   PDP_ERR_INTERNAL = -5,
+  PDP_ERR_NEEDS_SYNC = -6, /* pdp_get_status: an asynchronous call needed the generic path; redo it without
+                              PDP_BOUND_ASYNC */
+};
+
+/* pdp_bound_params.flags */
+enum {
+  /* No host synchronisation at all: the call only enqueues work on `stream` (it can be captured in a
+   * hipGraph).  Errors and statistics are read with pdp_get_status after the stream has drained.  An
+   * input that needs the generic path (privacy ids with more rows than the wave kernels hold) is not
+   * completed: pdp_get_status returns PDP_ERR_NEEDS_SYNC. */
+  PDP_BOUND_ASYNC = 1,
 };
 
 /* Metric bitmask (aggregate_params.py:54-65). */
@@ -117,6 +128,8 @@ typedef struct pdp_bound_params {
   int32_t debug_force_fallback;             /* testing: route every bucket through the
                                                generic sorted-stream path */
   int32_t reserved;                         /* testing: debug flags (pdp_ctx_set_debug); 0 */
+  int32_t flags;                            /* PDP_BOUND_* */
+  int32_t reserved2;
 } pdp_bound_params;
 
 /* Dense per-partition accumulators [num_partitions] (device).  row_count is the
@@ -174,7 +187,12 @@ int pdp_workspace_size(const pdp_columns* cols, const pdp_bound_params* bp, size
  * enough rows per privacy id the library first drops, after one bucket
  * radix pass, the rows of partitions their privacy id cannot keep (the L0
  * pre-filter); the result is identical either way, and
- * pdp_get_stats reports the surviving rows in filter_rows. */
+ * pdp_get_stats reports the surviving rows in filter_rows.
+ * Stream-ordered: the kernels read every intermediate count from device
+ * memory, so the call waits for the stream once, at the end, to return the
+ * status (none with PDP_BOUND_ASYNC).  An input that needs the generic path
+ * takes one more wait after the bounding kernels (the context then starts
+ * that way until an input no longer needs it). */
 int pdp_bound_accumulate(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp,
                          const pdp_accumulators* acc, void* workspace, size_t workspace_bytes,
                          void* stream);
@@ -408,9 +426,15 @@ typedef struct pdp_stats {
   int64_t k4_slots;            /* K4: pair slots written by K2 (+ generic-path groups); 0: K4 off */
   int64_t k4_pairs;            /* K4: (pid, pk) pair records reduced */
   int32_t k4_passes;           /* K4: radix passes on the partition block */
-  int32_t reserved_;
+  int32_t host_waits;          /* times the call waited for its stream (1: the final status copy;
+                                  0 with PDP_BOUND_ASYNC; more when the generic path ran) */
 } pdp_stats;
 int pdp_get_stats(pdp_ctx* ctx, pdp_stats* out);
+
+/* Status of the last pdp_bound_accumulate(_partials) on ctx, for PDP_BOUND_ASYNC calls: call after the
+ * stream they were enqueued on has drained (reads the context's device status block).  *call_status = 0,
+ * or the PDP_ERR_* code the call would have returned synchronously, or PDP_ERR_NEEDS_SYNC. */
+int pdp_get_status(pdp_ctx* ctx, int32_t* call_status);
 
 /* Per-stage device timing with hipEvents recorded on the launch stream (for
  * bench.py's roofline).  Stages: */

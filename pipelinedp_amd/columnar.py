@@ -50,6 +50,54 @@ class EncodedColumns:
     value: Optional[np.ndarray]
     num_privacy_ids: int
     partition_keys: list
+    # multi-rank: the rows' privacy-id key hashes, not yet dense ids -- World.exchange_by_key_hash
+    # moves every row to the rank owning its hash and numbers the privacy ids there
+    pid_hash: Optional[np.ndarray] = None
+
+
+def _canon(k) -> bytes:
+    """Canonical bytes of a privacy-id key, identical in every process (Python's
+    hash() is salted per process).  Keys equal as dict keys encode equally:
+    numpy scalars as their Python value, integral floats as ints."""
+    if isinstance(k, np.generic):
+        k = k.item()
+    if isinstance(k, bool):
+        return b"b1" if k else b"b0"
+    if isinstance(k, float) and k.is_integer():
+        k = int(k)
+    if isinstance(k, int):
+        return b"i" + str(k).encode()
+    if isinstance(k, str):
+        return b"s" + k.encode("utf-8", "surrogatepass")
+    if isinstance(k, float):
+        return b"f" + float.hex(k).encode()
+    if isinstance(k, bytes):
+        return b"y" + k
+    if isinstance(k, tuple):
+        return b"t(" + b",".join(_canon(x) for x in k) + b")"
+    if k is None:
+        return b"n"
+    return b"r" + repr(k).encode()
+
+
+def key_hashes(keys) -> np.ndarray:
+    """64-bit hash (int64) of each key: blake2b of its canonical bytes."""
+    import hashlib
+    out = np.empty(len(keys), dtype=np.int64)
+    for i, k in enumerate(keys):
+        out[i] = int.from_bytes(hashlib.blake2b(_canon(k), digest_size=8).digest(), "little", signed=True)
+    return out
+
+
+def dense_ids_from_hashes(h):
+    """Privacy ids numbered by the ascending (signed) order of their key hash:
+    the numbering World.exchange_by_key_hash reproduces across ranks without
+    exchanging keys (ranks own contiguous hash ranges).  Distinct keys with
+    equal 64-bit hashes (probability ~U^2 / 2^65) share one privacy id: their
+    contributions are bounded together -- stricter bounding, never weaker
+    privacy."""
+    uniq, inv = np.unique(np.asarray(h, dtype=np.int64), return_inverse=True)
+    return inv.astype(np.int64).reshape(-1), len(uniq)
 
 
 def _factorize(values):
@@ -95,9 +143,17 @@ def encode_rows(rows, extractors, public_partitions=None, need_pid=True, need_va
     ids [0, len(public)); rows of other partitions get -1 (dropped, like
     ``_drop_not_public_partitions`` dp_engine.py:283-293).  Without public
     partitions ids follow first appearance.  With a multi-rank ``world``
-    (``distributed.World``) the partition and privacy-id dictionaries are
-    agreed across ranks (``_global_keys``), so dense ids mean the same key
-    on every rank.
+    (``distributed.World``) the partition dictionary is agreed across ranks
+    (``_global_keys``: dense partition ids mean the same key on every rank,
+    which the reduce-scatter of [P] partials needs).
+
+    Privacy ids are numbered by their key hash (``dense_ids_from_hashes``),
+    in one process and across ranks alike, so the sampling (keyed by the
+    dense id) is the same whatever the world size.  With a multi-rank world
+    no privacy-id key leaves its rank: the rows carry their key hashes
+    (``pid_hash``), and ``World.exchange_by_key_hash`` moves them to the rank
+    owning the hash (the reference's group-by-privacy-id shuffle,
+    pipeline_backend.py:476-485) and numbers them there.
     """
     rows = rows if isinstance(rows, list) else list(rows)
     multi = world is not None and world.size > 1
@@ -110,22 +166,22 @@ def encode_rows(rows, extractors, public_partitions=None, need_pid=True, need_va
         pk = _index_of(keys, pk_raw)
     else:
         pk, keys = _factorize(pk_raw) if rows else (np.zeros(0, np.int64), [])
-    pid, U = None, 0
+    pid, U, pid_hash = None, 0, None
     if need_pid:
         pid_raw = [extractors.privacy_id_extractor(r) for r in rows]
-        if multi:
-            pid_keys = _global_keys(_unique_in_order(pid_raw), world)
-            pid = _index_of(pid_keys, pid_raw)
-            U = len(pid_keys)
-        elif rows:
-            pid, uniq = _factorize(pid_raw)
-            U = len(uniq)
+        if rows:
+            codes, uniq = _factorize(pid_raw)  # hash each distinct key once
+            h = key_hashes(uniq)[codes]
         else:
-            pid = np.zeros(0, np.int64)
+            h = np.zeros(0, np.int64)
+        if multi:
+            pid_hash = h
+        else:
+            pid, U = dense_ids_from_hashes(h)
     value = None
     if need_value:
         value = np.asarray([extractors.value_extractor(r) for r in rows], dtype=np.float64)
-    return EncodedColumns(pid, pk, value, U, keys)
+    return EncodedColumns(pid, pk, value, U, keys, pid_hash)
 
 
 def remap_public(pk, partition_keys, num_partitions, public_partitions):

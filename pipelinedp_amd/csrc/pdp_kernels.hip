@@ -81,7 +81,8 @@ enum Counter {
   kCtrNDropped = 15,  // rows of non-public partitions seen by k_filter
   kCtrK4In = 16,      // K4: records in the first pair pass's input (slots + generic-path pairs)
   kCtrK4Pairs = 17,   // K4: (pid, pk) pair records (non-empty slots)
-  kCtrTile0 = 18,  // 18..63 tile claim counters, one per onesweep launch
+  kCtrK4Chunk = 18,   // K4: pair records per reduce chunk (k4_total: ~1024 chunks, 4096 .. kK4Chunk)
+  kCtrTile0 = 19,  // 19..63 tile claim counters, one per onesweep launch
 };
 
 struct __align__(16) Rec {
@@ -249,7 +250,8 @@ constexpr int kDebugAnaNpartAtomics = 32;   // utility analysis: n_partitions by
 constexpr int kDebugAnaPack = 64;           // utility analysis: separate pack kernel before the sort
 constexpr int kDebugAnaFlags = 128;         // utility analysis: round-3 per-row flags + scan pair extraction
 constexpr int kDebugAnaSelLds = 256;        // utility analysis: round-3 per-regime selection kernels
-constexpr int kDebugK4TileScan = 1024;      // K4 pair passes by reduce-then-scan
+constexpr int kDebugDevOcc3 = 512;          // device-sized look-back passes at 3 blocks per CU (spills)
+constexpr int kDebugK4TileScan = 1024;      // K4 pair passes by reduce-then-scan (unused since round 5)
 // Timing ablations whose results are invalid: accepted only by a -DPDP_DEBUG_BUILD library.
 constexpr int kAblationFlags = kDebugSortOnly | kDebugNoLookback | kDebugLinearWrite | kDebugNoScatter |
                                kDebugNoAtomics | kDebugWalkOnly | kDebugNoLinf | kDebugNoSums | kDebugFilterTiming;
@@ -398,13 +400,16 @@ __device__ __forceinline__ Rec ana_rec(int64_t a, int64_t b, double v, const Key
 // MODE 0: records; 1: SoA columns (rows out of range dropped); 2: SoA columns of the utility
 // analysis (the records k_ana_pack would write: {pk, pid}, rows out of range as the all-ones
 // key that sorts last, pdp_analysis.inc)
+// n_dev != null: the row count is *n_dev (device memory; n is then an upper bound).
 template <int MODE>
 __global__ __launch_bounds__(kThreads) void k_histogram(const int64_t* __restrict__ pid,
                                                         const int64_t* __restrict__ pk,
                                                         const Rec* __restrict__ rin, int64_t n,
                                                         KeySpec ks, unsigned long long* __restrict__ hist,
-                                                        unsigned long long* __restrict__ counters) {
+                                                        unsigned long long* __restrict__ counters,
+                                                        const unsigned long long* __restrict__ n_dev) {
   __shared__ unsigned int sh[kMaxPasses * kHist];
+  if (n_dev) n = (int64_t)*n_dev;
   for (int i = threadIdx.x; i < kMaxPasses * kHist; i += kThreads) sh[i] = 0;
   __syncthreads();
   unsigned int invalid = 0;
@@ -677,8 +682,9 @@ __global__ __launch_bounds__(kThreads) void k_tile_bases(unsigned int* __restric
 __global__ __launch_bounds__(kThreads) void k_offsets(const unsigned long long* __restrict__ hist,
                                                       unsigned long long* __restrict__ off, int passes,
                                                       int64_t n, unsigned long long* __restrict__ counters,
-                                                      int n_slot) {
+                                                      int n_slot, const unsigned long long* __restrict__ n_dev) {
   __shared__ unsigned long long s_tmp[4];
+  if (n_dev) n = (int64_t)*n_dev;
   for (int p = 0; p < passes; ++p) {
     const unsigned long long v = hist[p * kHist + threadIdx.x];
     unsigned long long tot;
@@ -753,8 +759,11 @@ __device__ __forceinline__ uint32_t xcd_tile(uint32_t b, uint32_t nwg) {
 // records in (K2's slots, then the generic path's pairs after `split`) and out.
 // ANA (with SOA): the utility analysis' first pass -- the columns become the {pk, pid, value} records of
 // ana_rec (k_ana_pack fused in); no row is dropped (out-of-range rows carry the all-ones key).
+// Returns false when the claimed tile lies beyond the row count (the block is done): the look-back
+// wrappers loop over tiles claimed in order, so a grid smaller than the tile count (sized from a host
+// upper bound while the row count lives in device memory) covers every tile.
 template <bool SOA, bool TAG = false, int P12 = 0, bool ANA = false>
-__device__ __forceinline__ void onesweep_body(
+__device__ __forceinline__ bool onesweep_body(
     const int64_t* __restrict__ pid, const int64_t* __restrict__ pk, const double* __restrict__ val,
     const Rec* __restrict__ rin, Rec* __restrict__ rout, int64_t n_in,
     const unsigned long long* __restrict__ counters_n, int n_slot, KeySpec ks, int pass,
@@ -787,8 +796,11 @@ __device__ __forceinline__ void onesweep_body(
   // prefetch this tile's digit bases (their latency hides behind the loads)
   const unsigned int tb = (tile_base && t < 256) ? tile_base[tile * 256 + t] : 0u;
   const int64_t n_eff = SOA ? n_in : (int64_t)counters_n[n_slot];
+  // split = -(len(rin2)) - 1 (K4's first pass): rin holds the first n_eff - len(rin2) records, a count
+  // that lives in device memory
+  if (split < 0) split += n_eff + 1;
   const int64_t tile_start = tile * kTile;
-  if (tile_start >= n_eff) return;
+  if (tile_start >= n_eff) return false;
   const int radix_bits = ks.bits[pass];
   const int radix = 1 << radix_bits;
 
@@ -1095,6 +1107,7 @@ __device__ __forceinline__ void onesweep_body(
     atomicAdd(&counters[kCtrSweepTiles], 1ull);
   }
   (void)radix_bits;
+  return true;
 }
 
 // Distinct symbols per use, so rocprofv3 --stats (which truncates template
@@ -1110,9 +1123,22 @@ __device__ __forceinline__ void onesweep_body(
 #define PDP_ONESWEEP_PASS                                                                                  \
   pid, pk, val, rin, rout, n_in, counters_n, n_slot, ks, pass, off, status, epoch, counters, tile_slot,    \
       tile_base, tag_out, tag_lo, rin2, split
-// records -> records (passes >= 1 of the pid sort, survivor sort, generic path)
+// Launches whose tile count the host knows run one tile per block.  The passes over a row count that
+// lives in device memory (the survivor sort, K4's pair passes) loop over tiles claimed in order, so a
+// grid sized from a host bound covers every tile.  The loop costs registers (round 5: 80-108 B of
+// scratch at 3 blocks per CU; none at 2), so only those kernels have it, at 2 blocks per CU (debug flag
+// DEV_OCC3: 3).
+#define PDP_ONESWEEP_LOOP(...)                         \
+  while (__VA_ARGS__(PDP_ONESWEEP_PASS) && !tile_base) \
+    __syncthreads();
+// records -> records (passes >= 1 of the pid sort, generic path, utility analysis)
 __global__ __launch_bounds__(kThreads, PDP_OS_OCC) void k_onesweep(PDP_ONESWEEP_ARGS) {
   onesweep_body<false, false>(PDP_ONESWEEP_PASS);
+}
+// ... over a device-side record count (the L0 pre-filter's survivors)
+template <int OCC>
+__global__ __launch_bounds__(kThreads, OCC) void k_onesweep_dev(PDP_ONESWEEP_ARGS) {
+  PDP_ONESWEEP_LOOP(onesweep_body<false, false>)
 }
 // SoA columns -> records (first pass of the pid sort, non-public rows dropped)
 __global__ __launch_bounds__(kThreads, PDP_OS_OCC) void k_sort_first(PDP_ONESWEEP_ARGS) {
@@ -1126,17 +1152,61 @@ __global__ __launch_bounds__(kThreads, PDP_OS_OCC) void k_ana_sort_first(PDP_ONE
 __global__ __launch_bounds__(kThreads, PDP_OS_OCC) void k_bucket_pass(PDP_ONESWEEP_ARGS) {
   onesweep_body<true, true>(PDP_ONESWEEP_PASS);
 }
-// K4 pair records by partition block (pdp_reduce.inc)
-__global__ __launch_bounds__(kThreads, PDP_OS_OCC) void k_pair_pass(PDP_ONESWEEP_ARGS) {
-  onesweep_body<false, false>(PDP_ONESWEEP_PASS);
+// K4 pair records by partition block (pdp_reduce.inc); device-side record counts
+template <int OCC>
+__global__ __launch_bounds__(kThreads, OCC) void k_pair_pass(PDP_ONESWEEP_ARGS) {
+  PDP_ONESWEEP_LOOP(onesweep_body<false, false>)
 }
 // ... with 12-byte pair records (K2 writes its slots in that form)
-__global__ __launch_bounds__(kThreads, PDP_OS_OCC) void k_pair_pass12(PDP_ONESWEEP_ARGS) {
-  onesweep_body<false, false, 2>(PDP_ONESWEEP_PASS);
+template <int OCC>
+__global__ __launch_bounds__(kThreads, OCC) void k_pair_pass12(PDP_ONESWEEP_ARGS) {
+  PDP_ONESWEEP_LOOP(onesweep_body<false, false, 2>)
 }
 // ... whose first pass reads K2's split slots (keys, then the values of the non-empty ones)
-__global__ __launch_bounds__(kThreads, PDP_OS_OCC) void k_pair_pass12s(PDP_ONESWEEP_ARGS) {
-  onesweep_body<false, false, 3>(PDP_ONESWEEP_PASS);
+template <int OCC>
+__global__ __launch_bounds__(kThreads, OCC) void k_pair_pass12s(PDP_ONESWEEP_ARGS) {
+  PDP_ONESWEEP_LOOP(onesweep_body<false, false, 3>)
+}
+
+// Clears the look-back status words of the tiles of *rows_dev + add rows (a row count that lives in
+// device memory: the survivor sort, the K4 pair passes); grid-stride.
+__global__ __launch_bounds__(kThreads) void k_status_clear(unsigned long long* __restrict__ status,
+                                                           const unsigned long long* __restrict__ rows_dev, int64_t add) {
+  const int64_t rows = (int64_t)*rows_dev + add;
+  const int64_t words = (rows + kTile - 1) / kTile * kStatusStride;
+  for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < words; i += (int64_t)gridDim.x * kThreads)
+    status[i] = 0ull;
+}
+
+// Zeroes `words` 8-byte words (grid-stride).  The aggregate path clears its buffers with this kernel
+// rather than hipMemsetAsync, so a call captured in a hipGraph (PDP_BOUND_ASYNC) holds kernel nodes
+// only.
+__global__ __launch_bounds__(kThreads) void k_zero64(unsigned long long* __restrict__ p, int64_t words) {
+  for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < words; i += (int64_t)gridDim.x * kThreads)
+    p[i] = 0ull;
+}
+
+// End of a pdp_bound_accumulate call: the counters the host needs (errors, the generic-path request,
+// statistics) -> the context's device status block (kStat*), read back by ONE copy (or, for an
+// asynchronous call, by pdp_get_status after the stream has drained).
+enum StatWord {
+  kStatErr = 0, kStatInvalid, kStatRanges, kStatFull, kStatKeptRows, kStatSurvivors, kStatK4Slots, kStatK4Pairs,
+  kStatSweep0, kStatSweepTiles = kStatSweep0 + 4, kStatBig, kStatWords = 16
+};
+__global__ void k_latch(const unsigned long long* __restrict__ counters, unsigned long long* __restrict__ st) {
+  if (threadIdx.x == 0) {
+    st[kStatErr] = counters[kCtrErr];
+    st[kStatInvalid] = counters[kCtrInvalid];
+    st[kStatRanges] = counters[kCtrNRanges];
+    st[kStatFull] = counters[kCtrFull];
+    st[kStatKeptRows] = counters[kCtrNKept] - counters[kCtrNDropped];
+    st[kStatSurvivors] = counters[kCtrNSurv];
+    st[kStatK4Slots] = counters[kCtrK4In];
+    st[kStatK4Pairs] = counters[kCtrK4Pairs];
+    for (int i = 0; i < 4; ++i) st[kStatSweep0 + i] = counters[kCtrSweepCycles + i];
+    st[kStatSweepTiles] = counters[kCtrSweepTiles];
+    st[kStatBig] = counters[kCtrNBig];
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1766,6 +1836,16 @@ int grid_for(int64_t n, int threads, int cap = 4096) {
   return (int)g;
 }
 
+// hipMemsetAsync(p, 0, bytes) as a kernel (k_zero64): p 8-byte aligned, bytes a multiple of 8.
+hipError_t zero_async(void* p, size_t bytes, hipStream_t stream) {
+  if (bytes == 0) return hipSuccess;
+  if (((uintptr_t)p & 7u) || (bytes & 7u)) return hipMemsetAsync(p, 0, bytes, stream);
+  const int64_t words = (int64_t)(bytes / 8);
+  hipLaunchKernelGGL(k_zero64, dim3(grid_for(words, kThreads, 4096)), dim3(kThreads), 0, stream,
+                     (unsigned long long*)p, words);
+  return hipGetLastError();
+}
+
 struct Layout {
   size_t recs_a, recs_b, recs_c, hist, off, counters, status, ranges, big, tags, tag_lo, keep, k4rep, k4s, total;
   int64_t tiles;
@@ -1857,6 +1937,14 @@ SegParams make_seg(const pdp_bound_params* bp, int low, int pkb, bool has_value)
 struct pdp_ctx {
   int device = 0;
   int debug = 0;  // pdp_ctx_set_debug: alternative-form flags OR-ed into every call (testing)
+  int cur_debug = 0;  // the running call's flags (ctx->debug | pdp_bound_params.reserved)
+  // device status block of the last pdp_bound_accumulate(_partials) (k_latch, kStatWords words)
+  unsigned long long* dstat = nullptr;
+  bool dstat_pending = false;  // an asynchronous call wrote it: pdp_get_status / pdp_get_stats decode it
+  bool last_filter = false, last_k4 = false;
+  // the last call needed the generic path (overflowing / tied segments): the next one syncs after K2
+  // instead of running K4 first and redoing the call
+  bool careful = false;
   unsigned int tile_slot = kCtrTile0;  // next free onesweep tile-claim counter
   bool prof = false;
   struct ProfRec {
@@ -1956,13 +2044,28 @@ int env_int(const char* name, int def);
 // read as published status words -> wrong digit bases -> out-of-range scatter.
 int next_epoch(pdp_ctx* ctx, hipStream_t stream, unsigned long long* status, size_t status_bytes) {
   if (ctx->status_at != (void*)status || ctx->epoch >= 0xFFFE || status_bytes > ctx->status_ok) {
-    HIP_TRY(hipMemsetAsync(status, 0, status_bytes, stream));
+    HIP_TRY(zero_async(status, status_bytes, stream));
     ctx->status_at = status;
     ctx->status_ok = status_bytes;
     ctx->epoch = 0;
   }
   ++ctx->epoch;
   return 0;
+}
+
+// next_epoch for passes whose row count lives in device memory (*rows_dev + add): the clear is a
+// kernel sized by that count.  `fresh`: the first pass of a group (its tiles may exceed what earlier
+// passes of this call cleared).
+constexpr unsigned kPersistGrid = 2048;  // look-back launches over a device row count: blocks loop over tiles
+void next_epoch_dev(pdp_ctx* ctx, hipStream_t stream, unsigned long long* status, const unsigned long long* rows_dev,
+                    int64_t add, bool fresh) {
+  if (fresh || ctx->status_at != (void*)status || ctx->epoch >= 0xFFFE) {
+    hipLaunchKernelGGL(k_status_clear, dim3(1024), dim3(kThreads), 0, stream, status, rows_dev, add);
+    ctx->status_at = status;
+    ctx->status_ok = 0;  // a later host-sized pass clears what it needs
+    ctx->epoch = 0;
+  }
+  ++ctx->epoch;
 }
 
 int scan_inplace(long long* a, int64_t n, hipStream_t stream) {
@@ -2012,11 +2115,14 @@ void tile_scan(const TileScan& ts, const unsigned long long* off_pass, hipStream
 }
 
 // LSD sort of `m` records (a <-> b ping-pong) by the passes of `ks`; the
-// sorted array pointer is returned in *out.
+// sorted array pointer is returned in *out.  m_dev != null: the record count
+// is *m_dev (device memory, e.g. the pre-filter's survivors) and m an upper
+// bound -- no host round trip; the passes run on a persistent look-back grid.
 int sort_recs(pdp_ctx* ctx, Rec* a, Rec* b, int64_t m, const KeySpec& ks, unsigned long long* hist,
               unsigned long long* off, unsigned long long* counters, unsigned long long* status, size_t status_bytes,
               void* ws, hipStream_t stream, Rec** out, int stage = PDP_STAGE_GENERIC,
-              const int64_t* soa_pid = nullptr, const int64_t* soa_pk = nullptr, const double* soa_val = nullptr) {
+              const int64_t* soa_pid = nullptr, const int64_t* soa_pk = nullptr, const double* soa_val = nullptr,
+              const unsigned long long* m_dev = nullptr) {
   // soa_pk != null: the utility analysis' rows, packed by the histogram and the first pass themselves
   // (k_histogram<2>, k_ana_sort_first); `a` is not read
   if (m <= 0 || ks.passes == 0) {
@@ -2025,30 +2131,33 @@ int sort_recs(pdp_ctx* ctx, Rec* a, Rec* b, int64_t m, const KeySpec& ks, unsign
   }
   if (ks.passes > kMaxPasses) return fail(PDP_ERR_INTERNAL, "too many radix passes");
   if (ctx->tile_slot + ks.passes > kNumCounters) {
-    HIP_TRY(hipMemsetAsync(counters + kCtrTile0, 0, (kNumCounters - kCtrTile0) * 8, stream));
+    HIP_TRY(zero_async(counters + kCtrTile0, (kNumCounters - kCtrTile0) * 8, stream));
     ctx->tile_slot = kCtrTile0;
   }
-  HIP_TRY(hipMemsetAsync(hist, 0, kMaxPasses * kHist * 8, stream));
+  HIP_TRY(zero_async(hist, kMaxPasses * kHist * 8, stream));
   ProfScope prof_generic(ctx, stage, stream);
   if (soa_pk)
     hipLaunchKernelGGL(k_histogram<2>, dim3(grid_for(m, kThreads, 2048)), dim3(kThreads), 0, stream, soa_pid, soa_pk,
-                       (const Rec*)nullptr, m, ks, hist, counters);
+                       (const Rec*)nullptr, m, ks, hist, counters, m_dev);
   else
     hipLaunchKernelGGL(k_histogram<0>, dim3(grid_for(m, kThreads, 2048)), dim3(kThreads), 0, stream,
-                       (const int64_t*)nullptr, (const int64_t*)nullptr, a, m, ks, hist, counters);
+                       (const int64_t*)nullptr, (const int64_t*)nullptr, a, m, ks, hist, counters, m_dev);
   hipLaunchKernelGGL(k_offsets, dim3(1), dim3(kThreads), 0, stream, hist, off, ks.passes, m, counters,
-                     (int)kCtrNGeneric);
+                     (int)kCtrNGeneric, m_dev);
   Rec* src = a;
   Rec* dst = b;
   const int64_t tiles = (m + kTile - 1) / kTile;
   // decoupled look-back passes (no tile-count upsweeps): c3 survivor sort 2.15 -> 2.02 ms, c5 (pk, pid)
   // sort 7.26 -> 6.48 ms (same box); PDP_SORT_TILESCAN=1 restores reduce-then-scan
-  const bool rts = use_tile_scan(m, 0) && (ctx->debug & kDebugSortTileScan) != 0;
+  const bool rts = use_tile_scan(m, 0) && (ctx->cur_debug & kDebugSortTileScan) != 0 && !m_dev;
+  const unsigned grid = m_dev ? (unsigned)std::min<int64_t>(tiles, kPersistGrid) : (unsigned)tiles;
   for (int p = 0; p < ks.passes; ++p) {
     const unsigned int* bases = nullptr;
     // the fused first pass of the utility analysis reads the SoA columns: its tile counts would need
     // them too, so it always runs by look-back (k_tile_counts reads records)
-    if (rts && !(soa_pk && p == 0)) {
+    if (m_dev) {
+      next_epoch_dev(ctx, stream, status, m_dev, 0, p == 0);
+    } else if (rts && !(soa_pk && p == 0)) {
       const TileScan ts = tile_scan_bufs(ctx, status, tiles);
       hipLaunchKernelGGL(k_tile_counts, dim3(grid_for(tiles, 1, 4096)), dim3(kThreads), 0, stream, src, counters,
                          (int)kCtrNGeneric, ks, p, tiles, ts.tile_cnt);
@@ -2059,7 +2168,8 @@ int sort_recs(pdp_ctx* ctx, Rec* a, Rec* b, int64_t m, const KeySpec& ks, unsign
       if (rc) return rc;
     }
     const bool soa = soa_pk && p == 0;
-    hipLaunchKernelGGL(soa ? k_ana_sort_first : k_onesweep, dim3((unsigned)tiles), dim3(kThreads), 0, stream,
+    auto dev_kern = (ctx->cur_debug & kDebugDevOcc3) ? k_onesweep_dev<3> : k_onesweep_dev<2>;
+    hipLaunchKernelGGL(soa ? k_ana_sort_first : m_dev ? dev_kern : k_onesweep, dim3(grid), dim3(kThreads), 0, stream,
                        soa ? soa_pid : (const int64_t*)nullptr, soa ? soa_pk : (const int64_t*)nullptr,
                        soa ? soa_val : (const double*)nullptr, soa ? (const Rec*)nullptr : src, dst, m,
                        counters, (int)kCtrNGeneric, ks, p, off + p * kHist, status, ctx->epoch, counters,
@@ -2100,6 +2210,12 @@ KeySpec composite_spec(int mode, int hi_bits, int lo_bits, int pkb, uint64_t U, 
   return ks;
 }
 
+// Every wait of pdp_bound_accumulate for its stream goes through here (pdp_stats.host_waits).
+hipError_t host_wait(pdp_ctx* ctx, hipStream_t stream) {
+  ++ctx->stats.host_waits;
+  return hipStreamSynchronize(stream);
+}
+
 // `sorted` is only read (gather); `alt` is the generic sort's second buffer
 // (== sorted on the single-config path, a third buffer in a sweep so the
 // sorted rows survive for the next configuration).  K4 (sp.k4x != null): the
@@ -2136,7 +2252,7 @@ int run_generic(pdp_ctx* ctx, const Rec* sorted, Rec* spare, Rec* alt, const std
   HIP_TRY(hipMemcpyAsync(d_rdst, rdst.data(), nr * sizeof(long long), hipMemcpyHostToDevice, stream));
   hipLaunchKernelGGL(k_gather_ranges, dim3(grid_for(total, kThreads)), dim3(kThreads), 0, stream, sorted, spare,
                      d_rsrc, d_rdst, nr, total);
-  HIP_TRY(hipStreamSynchronize(stream));  // host vectors go out of scope
+  HIP_TRY(host_wait(ctx, stream));  // host vectors go out of scope
 
   // 1) rows by (pid, pk), stable (input order within a group)
   Rec* r = nullptr;
@@ -2159,7 +2275,7 @@ int run_generic(pdp_ctx* ctx, const Rec* sorted, Rec* spare, Rec* alt, const std
   long long ngroups = 0, npids = 0;
   HIP_TRY(hipMemcpyAsync(&ngroups, gsc + (total - 1), 8, hipMemcpyDeviceToHost, stream));
   HIP_TRY(hipMemcpyAsync(&npids, psc + (total - 1), 8, hipMemcpyDeviceToHost, stream));
-  HIP_TRY(hipStreamSynchronize(stream));
+  HIP_TRY(host_wait(ctx, stream));
 
   // 2) L_inf ranks: sort (group, row priority, row) -> rank within group.
   Rec *x1, *x2;
@@ -2200,7 +2316,7 @@ int run_generic(pdp_ctx* ctx, const Rec* sorted, Rec* spare, Rec* alt, const std
   }
   unsigned long long* big = nullptr;  // [count, group ids]: kept groups over kBigGroupRows rows
   HIP_TRY(scratch.alloc((void**)&big, (size_t)(total / kBigGroupRows + 2) * 8));
-  HIP_TRY(hipMemsetAsync(big, 0, 8, stream));
+  HIP_TRY(zero_async(big, 8, stream));
   hipLaunchKernelGGL(k_stream_groups, dim3(ggr), dim3(kThreads), 0, stream, r, gpos, grank, row_keep,
                      (int64_t)ngroups, sp, acc, big);
   hipLaunchKernelGGL(k_stream_big_groups, dim3((unsigned)std::min<int64_t>(total / kBigGroupRows + 1, 1024)),
@@ -2265,6 +2381,7 @@ double noise_scale(int kind, double eps, double delta, double l0, double linf) {
 }
 
 bool k4_enabled(int64_t n, bool sweep, int debug = 0);
+int decode_status(pdp_ctx* ctx, const unsigned long long* h);
 
 }  // namespace
 
@@ -2277,6 +2394,8 @@ const char* pdp_last_error(void) { return g_err.c_str(); }
 pdp_ctx* pdp_ctx_create(int device) {
   pdp_ctx* c = new pdp_ctx();
   c->device = device;
+  DeviceGuard dg(device);
+  if (!dg.ok || hipMalloc((void**)&c->dstat, kStatWords * 8) != hipSuccess) c->dstat = nullptr;
   return c;
 }
 
@@ -2288,6 +2407,7 @@ void pdp_ctx_destroy(pdp_ctx* ctx) {
   }
   for (auto e : ctx->pool) (void)hipEventDestroy(e);
   if (ctx->table_dev) (void)hipFree(ctx->table_dev);
+  if (ctx->dstat) (void)hipFree(ctx->dstat);
   delete ctx;
 }
 
@@ -2393,8 +2513,33 @@ int pdp_ctx_set_debug(pdp_ctx* ctx, int32_t flags) {
   return 0;
 }
 
+int pdp_get_status(pdp_ctx* ctx, int32_t* call_status) {
+  if (!ctx || !call_status) return fail(PDP_ERR_INVALID_ARG, "null argument");
+  *call_status = 0;
+  if (!ctx->dstat_pending) return 0;
+  DeviceGuard dg(ctx->device);
+  if (!dg.ok) return fail(PDP_ERR_HIP, "hipSetDevice failed");
+  unsigned long long h[kStatWords];
+  HIP_TRY(hipMemcpy(h, ctx->dstat, sizeof(h), hipMemcpyDeviceToHost));
+  ctx->dstat_pending = false;
+  const std::string prev = g_err;
+  int rc = decode_status(ctx, h);
+  if (!rc && (h[kStatRanges] || h[kStatFull])) {
+    rc = fail(PDP_ERR_NEEDS_SYNC, "the input needs the generic path: call again without PDP_BOUND_ASYNC");
+    ctx->careful = true;
+  }
+  *call_status = rc;
+  if (!rc) g_err = prev;
+  return 0;
+}
+
 int pdp_get_stats(pdp_ctx* ctx, pdp_stats* out) {
   if (!ctx || !out) return fail(PDP_ERR_INVALID_ARG, "null argument");
+  if (ctx->dstat_pending) {
+    int32_t st = 0;
+    if (int rc = pdp_get_status(ctx, &st)) return rc;
+    ctx->dstat_pending = true;  // the status stays readable by pdp_get_status
+  }
   *out = ctx->stats;
   return 0;
 }
@@ -2523,21 +2668,27 @@ K4Red k4_red(const K4Plan& k, const SegParams& sp, int64_t P, bool y) {
   return r;
 }
 
-// One K4 run: pair passes over [in_a (len_a) | in_b (len_b)] (ping-pong in
-// buf1 / buf2), then the chunked reduction into `acc` (y = the VARIANCE run).
-int k4_run(pdp_ctx* ctx, hipStream_t stream, const K4Plan& k, const K4Red& kr, bool y, const Rec* in_a,
-           int64_t len_a, const Rec* in_b, int64_t len_b, Rec* buf1, Rec* buf2, AccPtrs acc,
+// One K4 run: pair passes over [in_a | in_b (len_b)] (ping-pong in buf1 /
+// buf2), then the chunked reduction into `acc` (y = the VARIANCE run).  The
+// number of records of in_a lives in device memory (counters[a_slot]: K2's
+// slots; a_slot < 0: none) and upper_a bounds it, so nothing here waits for
+// the host: k4_total sets the first pass's input count and the reduce chunk,
+// the passes run on a persistent look-back grid and the reduction kernels
+// stride over their chunks.
+int k4_run(pdp_ctx* ctx, hipStream_t stream, const K4Plan& k, const K4Red& kr, bool y, const Rec* in_a, int a_slot,
+           int64_t upper_a, const Rec* in_b, int64_t len_b, Rec* buf1, Rec* buf2, AccPtrs acc,
            unsigned long long* off, unsigned long long* counters, unsigned long long* status, void* ws,
            unsigned long long* s_lo, unsigned long long* s_hi, unsigned int* s_fl, int64_t buf_cap,
            int64_t soa_a = 0, int64_t soa_b = 0) {
-  const int64_t total = len_a + len_b;
-  if (total == 0) return 0;
-  hipLaunchKernelGGL(k4_set_counter, dim3(1), dim3(64), 0, stream, counters, (int)kCtrK4In,
-                     (unsigned long long)total);
+  const int64_t upper = upper_a + len_b;
+  if (upper == 0) return 0;
+  // in_a's count: counters[a_slot], or exactly upper_a (a host count) when a_slot < 0
+  hipLaunchKernelGGL(k4_total, dim3(1), dim3(64), 0, stream, counters, a_slot,
+                     (unsigned long long)((a_slot < 0 ? upper_a : 0) + len_b));
   KeySpec ks{};
   ks.xcd_remap = 1;
   ks.mode = 6;
-  ks.cap = std::min<int64_t>(total, buf_cap);  // the pairs (< total) land in buf1 / buf2
+  ks.cap = buf_cap;  // the pairs (<= records) land in buf1 / buf2
   ks.soa_a = soa_a;
   ks.soa_b = soa_b;
   ks.low = kr.sh + (k.p12 ? k.cb : 0);  // 12-byte records: the block digit sits above the count bits
@@ -2546,71 +2697,76 @@ int k4_run(pdp_ctx* ctx, hipStream_t stream, const K4Plan& k, const K4Red& kr, b
     ks.shift[i] = k.shift[i];
     ks.bits[i] = k.bits[i];
   }
-  const int64_t tiles = (total + kTile - 1) / kTile;
-  const size_t status_bytes = (size_t)tiles * kStatusStride * 8;
+  const int64_t tiles = (upper + kTile - 1) / kTile;
+  const unsigned grid = (unsigned)std::min<int64_t>(tiles, kPersistGrid);
   const Rec* src = in_a;
   Rec* dst = buf1;
-  // decoupled look-back passes; PDP_K4_TILESCAN=1: reduce-then-scan (tile digit counts, scanned tile
-  // bases, tiles in XCD-contiguous runs) -- parity-green, but c4 pair passes 8.31 -> 8.60 ms with it
-  // (the counts re-read 8 GB of slots; same box r04i), c3 / c2 unchanged
-  const bool rts = use_tile_scan(total, 0) && (ctx->debug & kDebugK4TileScan) != 0;
   {
     ProfScope ps(ctx, PDP_STAGE_PAIR_PASS, stream);
     for (int p = 0; p < k.passes; ++p) {
       if (ctx->tile_slot >= kNumCounters) {
-        HIP_TRY(hipMemsetAsync(counters + kCtrTile0, 0, (kNumCounters - kCtrTile0) * 8, stream));
+        HIP_TRY(zero_async(counters + kCtrTile0, (kNumCounters - kCtrTile0) * 8, stream));
         ctx->tile_slot = kCtrTile0;
       }
       const int n_slot = p == 0 ? (int)kCtrK4In : (int)kCtrK4Pairs;
       const Rec* src2 = p == 0 ? in_b : (const Rec*)nullptr;
-      const int64_t split = p == 0 ? len_a : (int64_t)INT64_MAX;
-      const unsigned int* bases = nullptr;
-      if (rts) {
-        const TileScan ts = tile_scan_bufs(ctx, status, tiles);
-        auto cnt_kern = k.p12 ? k_pair_tile_counts<1> : k_pair_tile_counts<0>;
-        hipLaunchKernelGGL(cnt_kern, dim3(grid_for(tiles, 1, 4096)), dim3(kThreads), 0, stream, src, src2, split,
-                           counters, n_slot, ks, p, tiles, ts.tile_cnt);
-        tile_scan(ts, off + p * kHist, stream);
-        bases = ts.tile_cnt;
-      } else if (int rc = next_epoch(ctx, stream, status, status_bytes)) {
-        return rc;
-      }
-      auto pass_kern = k.p12 ? (p == 0 && k.soa ? k_pair_pass12s : k_pair_pass12) : k_pair_pass;
-      hipLaunchKernelGGL(pass_kern, dim3((unsigned)tiles), dim3(kThreads), 0, stream, (const int64_t*)nullptr,
+      // in_a's records come first and their count is device-side: -(len_b) - 1 makes the pass split at
+      // n_eff - len_b (onesweep_body); without in_b nothing is read from rin2
+      const int64_t split = p == 0 && in_b ? -len_b - 1 : (int64_t)INT64_MAX;
+      next_epoch_dev(ctx, stream, status, counters + kCtrK4In, 0, p == 0);
+      const bool o3 = (ctx->cur_debug & kDebugDevOcc3) != 0;
+      auto pass_kern = k.p12 ? (p == 0 && k.soa ? (o3 ? k_pair_pass12s<3> : k_pair_pass12s<2>)
+                                                : (o3 ? k_pair_pass12<3> : k_pair_pass12<2>))
+                             : (o3 ? k_pair_pass<3> : k_pair_pass<2>);
+      hipLaunchKernelGGL(pass_kern, dim3(grid), dim3(kThreads), 0, stream, (const int64_t*)nullptr,
                          (const int64_t*)nullptr, (const double*)nullptr, src, dst, (int64_t)0, counters, n_slot,
-                         ks, p, off + p * kHist, status, ctx->epoch, counters, (int)ctx->tile_slot++, bases,
-                         (uint32_t*)nullptr, (const uint32_t*)nullptr, src2, split);
+                         ks, p, off + p * kHist, status, ctx->epoch, counters, (int)ctx->tile_slot++,
+                         (const unsigned int*)nullptr, (uint32_t*)nullptr, (const uint32_t*)nullptr, src2, split);
       src = dst;
       dst = (dst == buf1) ? buf2 : buf1;
     }
   }
   HIP_TRY(hipGetLastError());
   ProfScope ps(ctx, PDP_STAGE_REDUCE, stream);
-  const int64_t chunks = (total + kr.chunk - 1) / kr.chunk;
-  const bool scratch = (y || kr.want_x) && chunks > 1;
+  K4Red kd = kr;
+  kd.chunk = 0;  // counters[kCtrK4Chunk] (k4_total)
+  const unsigned cgrid = (unsigned)std::min<int64_t>((upper + 4095) / 4096, 1024);
+  const bool scratch = y || kr.want_x;
   if (scratch)
-    hipLaunchKernelGGL(k.p12 ? k4_zero_shared<1> : k4_zero_shared<0>, dim3((unsigned)(chunks - 1)), dim3(kThreads), 0,
-                       stream, src, counters, kr.sh, kr.P, kr.chunk, s_lo, s_hi, s_fl, kr.cb);
-  // window of 2^sh partitions: 12 or 11 by k4_plan, 10 by PDP_K4_SH=10 (28 KiB of LDS: 4 workgroups per CU)
-  auto pick = [&](auto k12, auto k11, auto k10) { return kr.sh == kK4ShMax ? k12 : kr.sh == kK4ShMax - 1 ? k11 : k10; };
+    hipLaunchKernelGGL(k.p12 ? k4_zero_shared<1> : k4_zero_shared<0>, dim3(cgrid), dim3(kThreads), 0, stream, src,
+                       counters, kr.sh, kr.P, (int64_t)0, s_lo, s_hi, s_fl, kr.cb);
+  auto pick = [&](auto k12, auto k11) { return kr.sh == kK4ShMax ? k12 : k11; };
   decltype(&k4_reduce<true, kK4ShMax, 0>) kern;
   if (k.p12)
-    kern = y ? pick(k4_reduce<true, kK4ShMax, 1>, k4_reduce<true, kK4ShMax - 1, 1>, k4_reduce<true, kK4ShMax - 2, 1>)
-             : pick(k4_reduce<false, kK4ShMax, 1>, k4_reduce<false, kK4ShMax - 1, 1>,
-                    k4_reduce<false, kK4ShMax - 2, 1>);
+    kern = y ? pick(k4_reduce<true, kK4ShMax, 1>, k4_reduce<true, kK4ShMax - 1, 1>)
+             : pick(k4_reduce<false, kK4ShMax, 1>, k4_reduce<false, kK4ShMax - 1, 1>);
   else
-    kern = y ? pick(k4_reduce<true, kK4ShMax, 0>, k4_reduce<true, kK4ShMax - 1, 0>, k4_reduce<true, kK4ShMax - 2, 0>)
-             : pick(k4_reduce<false, kK4ShMax, 0>, k4_reduce<false, kK4ShMax - 1, 0>,
-                    k4_reduce<false, kK4ShMax - 2, 0>);
-  hipLaunchKernelGGL(kern, dim3((unsigned)chunks), dim3(kK4Threads), 0, stream, src, counters, kr, acc, s_lo, s_hi,
-                     s_fl);
+    kern = y ? pick(k4_reduce<true, kK4ShMax, 0>, k4_reduce<true, kK4ShMax - 1, 0>)
+             : pick(k4_reduce<false, kK4ShMax, 0>, k4_reduce<false, kK4ShMax - 1, 0>);
+  hipLaunchKernelGGL(kern, dim3(cgrid), dim3(kK4Threads), 0, stream, src, counters, kd, acc, s_lo, s_hi, s_fl);
   if (scratch) {
     auto fin = y ? (k.p12 ? k4_finalize<true, 1> : k4_finalize<true, 0>)
                  : (k.p12 ? k4_finalize<false, 1> : k4_finalize<false, 0>);
-    hipLaunchKernelGGL(fin, dim3((unsigned)(chunks - 1)), dim3(kThreads), 0, stream, src, counters, kr, acc, s_lo,
-                       s_hi, s_fl);
+    hipLaunchKernelGGL(fin, dim3(cgrid), dim3(kThreads), 0, stream, src, counters, kd, acc, s_lo, s_hi, s_fl);
   }
   HIP_TRY(hipGetLastError());
+  return 0;
+}
+
+// Status block (k_latch) -> ctx->stats and the call's return code.  The generic-path request
+// (ranges / full) is not an error here: the caller decides (redo the call, or PDP_ERR_NEEDS_SYNC).
+int decode_status(pdp_ctx* ctx, const unsigned long long* h) {
+  ctx->stats.kept_rows_in = (int64_t)h[kStatKeptRows];
+  ctx->stats.filter_rows = ctx->last_filter ? (int64_t)h[kStatSurvivors] : 0;
+  ctx->stats.k4_slots = ctx->last_k4 ? (int64_t)h[kStatK4Slots] : 0;
+  ctx->stats.k4_pairs = ctx->last_k4 ? (int64_t)h[kStatK4Pairs] : 0;
+  for (int i = 0; i < 4; ++i) ctx->stats.sweep_cycles[i] = (int64_t)h[kStatSweep0 + i];
+  ctx->stats.sweep_tiles = (int64_t)h[kStatSweepTiles];
+  if (h[kStatInvalid]) return fail(PDP_ERR_OUT_OF_RANGE, "privacy id or partition id out of range");
+  const unsigned long long err = h[kStatErr];
+  if (err & 4) return fail(PDP_ERR_INTERNAL, "K4 pair histogram disagrees with the pair records");
+  if (err & 2) return fail(PDP_ERR_INTERNAL, "K4 pair records not grouped by partition block");
+  if (err) return fail(PDP_ERR_INTERNAL, "radix look-back timed out");
   return 0;
 }
 
@@ -2618,9 +2774,21 @@ int k4_run(pdp_ctx* ctx, hipStream_t stream, const K4Plan& k, const K4Red& kr, b
 // pdp_bound_accumulate_sweep: K0/K1 sort the rows by privacy id ONCE (the
 // order does not depend on L0 / L_inf / clipping), then K2 (+ KF) runs per
 // configuration over the same sorted rows.
+//
+// Host round trips (stream-ordered, no host sync inside).  Every
+// count the kernels need lives in device memory (survivors, K2's slots, K4's
+// pairs and chunk) and every grid is sized from a host upper bound, so the
+// common path -- no privacy id routed to the generic path -- enqueues K0 ..
+// K4 without waiting, then copies the status block back ONCE at the end
+// (errors, statistics).  PDP_BOUND_ASYNC skips even that copy (the call can be
+// captured in a hipGraph; pdp_get_status reports afterwards).  The generic
+// path (KF: privacy ids of > 1024 rows in a wave kernel, tied priorities that
+// k_segments_big does not take) needs the host: when the final status asks
+// for it, the call is redone "careful" -- one sync after K2, KF, then K4 --
+// and the context remembers to start careful next time (ctx->careful).
 int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bps, int nconf,
                const pdp_accumulators* accps, void* workspace, size_t workspace_bytes, void* stream_, bool sweep,
-               const pdp_partials* parts = nullptr) {
+               const pdp_partials* parts = nullptr, int force_careful = 0) {
   if (!ctx || !cols || !bps || !accps) return fail(PDP_ERR_INVALID_ARG, "null argument");
   if (parts && (sweep || nconf != 1)) return fail(PDP_ERR_INVALID_ARG, "partials: one configuration, no sweep");
   if (nconf < 1) return fail(PDP_ERR_INVALID_ARG, "num_configs must be >= 1");
@@ -2667,22 +2835,36 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
   if (!bp->bounds_already_enforced && n > 0 && !cols->pid) return fail(PDP_ERR_INVALID_ARG, "pid column required");
   SegParams sp = sps[0];
   AccPtrs acc = accs[0];
+  const bool async = (bp->flags & PDP_BOUND_ASYNC) != 0;
+  ctx->cur_debug = sp.debug;
+  if (async && sweep) return fail(PDP_ERR_INVALID_ARG, "PDP_BOUND_ASYNC: one configuration, no sweep");
+  if (!ctx->dstat) return fail(PDP_ERR_HIP, "context status block not allocated (hipMalloc failed)");
+  const bool careful = !async && (force_careful || sweep || ctx->careful || bp->debug_force_fallback != 0);
+  const int32_t waits = force_careful ? ctx->stats.host_waits : 0;  // a redone call counts both passes
   ctx->stats = pdp_stats{};
+  ctx->stats.host_waits = waits;
   ctx->stats.bucket_low_bits = plan.low;
+  ctx->dstat_pending = false;
 
   for (const AccPtrs& a : accs) {
-    HIP_TRY(hipMemsetAsync(a.row_count, 0, (size_t)P * 8, stream));
-    if (a.count) HIP_TRY(hipMemsetAsync(a.count, 0, (size_t)P * 8, stream));
-    if (a.x) HIP_TRY(hipMemsetAsync(a.x, 0, (size_t)P * 8, stream));
-    if (a.y) HIP_TRY(hipMemsetAsync(a.y, 0, (size_t)P * 8, stream));
+    HIP_TRY(zero_async(a.row_count, (size_t)P * 8, stream));
+    if (a.count) HIP_TRY(zero_async(a.count, (size_t)P * 8, stream));
+    if (a.x) HIP_TRY(zero_async(a.x, (size_t)P * 8, stream));
+    if (a.y) HIP_TRY(zero_async(a.y, (size_t)P * 8, stream));
   }
   if (parts) {
     for (int64_t* t : {parts->x_hi, parts->x_lo, parts->y_hi, parts->y_lo, parts->nan})
-      if (t) HIP_TRY(hipMemsetAsync(t, 0, (size_t)P * 8, stream));
+      if (t) HIP_TRY(zero_async(t, (size_t)P * 8, stream));
   }
-  if (n == 0) return 0;
+  if (n == 0) {
+    HIP_TRY(zero_async(ctx->dstat, kStatWords * 8, stream));
+    ctx->dstat_pending = async;
+    return 0;
+  }
 
   const K4Plan k4 = k4_plan(bp, sp, n, P, sweep);
+  ctx->last_k4 = k4.on;
+  ctx->last_filter = false;
   if (parts && !k4.on) return fail(PDP_ERR_INVALID_ARG, "partials need the K4 reduction (num_rows < 2^32, PDP_K4 on)");
   const Layout L = layout_for(n, sweep, k4.on ? P : 0, sp.want_y != 0);
   if (!workspace || workspace_bytes < L.total) return fail(PDP_ERR_WORKSPACE, "workspace too small");
@@ -2695,8 +2877,26 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
   unsigned long long* status = (unsigned long long*)(ws + L.status);
   unsigned long long* ranges = (unsigned long long*)(ws + L.ranges);
   const size_t status_bytes = (size_t)L.tiles * kStatusStride * 8;
-  HIP_TRY(hipMemsetAsync(ws + L.hist, 0, L.status - L.hist, stream));  // hist, off, counters
+  HIP_TRY(zero_async(ws + L.hist, L.status - L.hist, stream));  // hist, off, counters
   ctx->tile_slot = kCtrTile0;
+  // End of the call: the status block, then (unless PDP_BOUND_ASYNC) ONE copy to the host.
+  // *redo: the generic path was needed and this pass did not run it.
+  auto finish = [&](bool generic_done, bool* redo) -> int {
+    hipLaunchKernelGGL(k_latch, dim3(1), dim3(64), 0, stream, counters, ctx->dstat);
+    HIP_TRY(hipGetLastError());
+    if (async) {
+      ctx->dstat_pending = true;
+      return 0;
+    }
+    unsigned long long h[kStatWords];
+    HIP_TRY(hipMemcpyAsync(h, ctx->dstat, sizeof(h), hipMemcpyDeviceToHost, stream));
+    HIP_TRY(host_wait(ctx, stream));
+    if (int rc = decode_status(ctx, h)) return rc;
+    const bool generic = h[kStatRanges] != 0 || h[kStatFull] != 0;
+    if (redo) *redo = generic && !generic_done;
+    ctx->careful = generic;
+    return 0;
+  };
   ctx->status_at = nullptr;  // first look-back pass of this call clears its status words (next_epoch)
   // K4 (pdp_reduce.inc): pair records into `slots` (+ the y slots), then pair passes + reduction
   unsigned int* k4rep = (unsigned int*)(ws + L.k4rep);
@@ -2719,19 +2919,14 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
       q.k4bits[i] = k4.bits[i];
     }
   };
-  // after K2 (+ KF): x run over [slots | generic-path pairs], then the y run (VARIANCE)
-  auto k4_finish = [&](const SegParams& q, const Rec* slots, int64_t nslots, const Rec* kfx, const Rec* kfy,
+  // after K2 (+ KF): x run over [slots | generic-path pairs], then the y run (VARIANCE).  The slot
+  // count is counters[slot] (device; slot < 0: exactly `upper` slots), at most `upper`.
+  auto k4_finish = [&](const SegParams& q, const Rec* slots, int slot, int64_t upper, const Rec* kfx, const Rec* kfy,
                        int64_t nkf, Rec* buf1, Rec* buf2) -> int {
     hipLaunchKernelGGL(k4_offsets, dim3(1), dim3(kThreads), 0, stream, k4rep, k4.passes, off, counters);
-    ctx->stats.k4_slots = nslots + nkf;
     ctx->stats.k4_passes = k4.passes;
+    // records per reduce chunk: counters[kCtrK4Chunk] (k4_total: ~1024 chunks, 4096 .. 32768)
     K4Red krx = k4_red(k4, q, P, false), kry = k4_red(k4, q, P, true);
-    {
-      // records per reduce workgroup: 32768, fewer for small inputs so that the reduction still has
-      // about 1024 workgroups (a rank's share of a multi-GPU step: c3 at 8 GPUs has ~8e6 slots)
-      const int64_t c = std::min<int64_t>(kK4Chunk, std::max<int64_t>(4096, (nslots + nkf) / 1024 / 4096 * 4096));
-      krx.chunk = kry.chunk = c;
-    }
     if (parts) {  // fixed-point export (multi-GPU partials)
       krx.fxh = (long long*)parts->x_hi;
       krx.fxl = (long long*)parts->x_lo;
@@ -2743,17 +2938,17 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
       kry.nan_inc = 1ull << 32;
     }
     const int64_t soa_a = q.k4soa, soa_b = k4.soa ? k4_soa_offset(nkf) : 0;
-    if (int rc = k4_run(ctx, stream, k4, krx, false, slots, nslots, kfx, nkf, buf1, buf2, acc, off, counters, status,
-                        workspace, k4lo, k4hi, k4fl, n, soa_a, soa_b))
+    if (int rc = k4_run(ctx, stream, k4, krx, false, slots, slot, upper, kfx, nkf, buf1, buf2, acc, off, counters,
+                        status, workspace, k4lo, k4hi, k4fl, n, soa_a, soa_b))
       return rc;
     if (q.want_y) {
-      if (int rc = k4_run(ctx, stream, k4, kry, true, k4y, nslots, kfy, nkf, buf1, buf2, acc, off, counters, status,
-                          workspace, k4lo, k4hi, k4fl, n, soa_a, soa_b))
+      if (int rc = k4_run(ctx, stream, k4, kry, true, k4y, slot, upper, kfy, nkf, buf1, buf2, acc, off, counters,
+                          status, workspace, k4lo, k4hi, k4fl, n, soa_a, soa_b))
         return rc;
     }
     return 0;
   };
-  if (k4.on) HIP_TRY(hipMemsetAsync(k4rep, 0, (size_t)kK4Rep * kK4MaxPasses * 256 * 4, stream));
+  if (k4.on) HIP_TRY(zero_async(k4rep, (size_t)kK4Rep * kK4MaxPasses * 256 * 4, stream));
 
   if (bp->bounds_already_enforced) {
     k4_attach(sp, recs_a);
@@ -2764,12 +2959,12 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
     }
     HIP_TRY(hipGetLastError());
     if (k4.on) {
-      if (int rc = k4_finish(sp, recs_a, n, nullptr, nullptr, 0, recs_b, recs_a)) return rc;
+      if (int rc = k4_finish(sp, recs_a, -1, n, nullptr, nullptr, 0, recs_b, recs_a)) return rc;
     }
-    unsigned long long inv = 0;
-    HIP_TRY(hipMemcpyAsync(&inv, counters + kCtrInvalid, 8, hipMemcpyDeviceToHost, stream));
-    HIP_TRY(hipStreamSynchronize(stream));
-    if (inv) return fail(PDP_ERR_OUT_OF_RANGE, "partition id >= num_partitions in input");
+    if (int rc = finish(true, nullptr)) {
+      if (rc == PDP_ERR_OUT_OF_RANGE) return fail(rc, "partition id >= num_partitions in input");
+      return rc;
+    }
     return 0;
   }
 
@@ -2799,6 +2994,7 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
   const FilterPlan fpl = filter_plan(n, U, bp, sp.debug, sweep, rts);
   uint32_t* tags = (uint32_t*)(ws + L.tags);
   uint32_t* tag_lo = (uint32_t*)(ws + L.tag_lo);
+  ctx->last_filter = fpl.on;
   if (fpl.on) {
     ks.mode = 4;
     ks.mult = fpl.mult;
@@ -2815,10 +3011,11 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
                          dim3(kThreads), 0, stream, cols->pid, cols->pk, n, ks, hist, ts.tile_cnt, counters);
     else
       hipLaunchKernelGGL(k_histogram<1>, dim3(grid_for(n, kThreads, 2048)), dim3(kThreads), 0, stream,
-                         cols->pid, cols->pk, (const Rec*)nullptr, n, ks, hist, counters);
+                         cols->pid, cols->pk, (const Rec*)nullptr, n, ks, hist, counters,
+                         (const unsigned long long*)nullptr);
   }
   hipLaunchKernelGGL(k_offsets, dim3(1), dim3(kThreads), 0, stream, hist, off, ks.passes, n, counters,
-                     (int)kCtrNKept);
+                     (int)kCtrNKept, (const unsigned long long*)nullptr);
   Rec* src = nullptr;
   Rec* dst = recs_a;
   // Passes >= 1 reduce-then-scan too (round 4): at c4 the two later passes took 2 x 5.03 ms by
@@ -2863,14 +3060,14 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
   Rec* sorted = src;
   Rec* spare = dst;
   if (sp.debug & kDebugSortOnly) {
-    HIP_TRY(hipStreamSynchronize(stream));
+    HIP_TRY(host_wait(ctx, stream));
     return 0;
   }
   int n_slot = kCtrNKept;  // counter holding the number of rows in `sorted`
   uint64_t n_sorted = (uint64_t)n;  // upper bound of that number (grid sizes)
   if (fpl.on) {
     // K1f: survivors of the bucket-sorted rows -> spare (input order per pid kept)
-    HIP_TRY(hipMemsetAsync(counters + kCtrNSurv, 0, 8, stream));
+    HIP_TRY(zero_async(counters + kCtrNSurv, 8, stream));
     {
       ProfScope ps(ctx, PDP_STAGE_FILTER, stream);
       hipLaunchKernelGGL(fpl.half ? k_filter<true> : k_filter<false>, dim3(256), dim3(kFiltThreads), 0, stream,
@@ -2880,10 +3077,6 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
                          (sp.debug & kDebugFilterTiming) != 0);
     }
     HIP_TRY(hipGetLastError());
-    unsigned long long m = 0;
-    HIP_TRY(hipMemcpyAsync(&m, counters + kCtrNSurv, 8, hipMemcpyDeviceToHost, stream));
-    HIP_TRY(hipStreamSynchronize(stream));
-    ctx->stats.filter_rows = (int64_t)m;
     // Survivors stably by pid & (2^low_bits - 1) only.  That groups every pid: within a bucket the
     // ids are distinct mod 2^low_bits (a bucket spans <= 2^low_bits ids), and rows of equal low bits
     // from different buckets stay in the order of their buckets' runs, because k_filter writes each
@@ -2897,17 +3090,16 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
       ++k2.passes;
     }
     ctx->stats.sort_passes += k2.passes;
-    if (m == 0) HIP_TRY(hipMemsetAsync(counters + kCtrNGeneric, 0, 8, stream));
+    // the survivor count stays on the device (counters[kCtrNSurv]): the sort and K2 are sized by n
     Rec* sa = spare;
     Rec* sb = sorted;
     Rec* out = nullptr;
-    int rc = sort_recs(ctx, sa, sb, (int64_t)m, k2, hist, off, counters, status, status_bytes, workspace, stream, &out,
-                       PDP_STAGE_SURVIVOR_SORT);
+    int rc = sort_recs(ctx, sa, sb, n, k2, hist, off, counters, status, status_bytes, workspace, stream, &out,
+                       PDP_STAGE_SURVIVOR_SORT, nullptr, nullptr, nullptr, counters + kCtrNSurv);
     if (rc) return rc;
     sorted = out;
     spare = (out == sa) ? sb : sa;
     n_slot = kCtrNGeneric;
-    n_sorted = m;
   }
 
   OvList ov{ranges, counters};
@@ -2926,7 +3118,7 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
     unsigned long long reset[kCtrSweepCycles] = {};
     reset[kCtrNKept] = n_kept;
     HIP_TRY(hipMemcpyAsync(counters, reset, sizeof(reset), hipMemcpyHostToDevice, stream));
-    HIP_TRY(hipStreamSynchronize(stream));
+    HIP_TRY(host_wait(ctx, stream));
   }
   {
     ProfScope ps(ctx, PDP_STAGE_BUCKETS, stream);
@@ -2970,13 +3162,35 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
       hipLaunchKernelGGL(k_segments, dim3((unsigned)seg_grid), dim3(kThreads), 0, stream, sorted, counters, n_slot,
                          sp, acc, ov, big, (int)bp->debug_force_fallback);
     }
+    // tied segments of <= kBigMax rows: from the overflow ranges to k_segments_big (not under
+    // debug_force_fallback, which tests the generic path itself)
+    if (!bp->debug_force_fallback)
+      hipLaunchKernelGGL(k_ranges_to_big, dim3(1), dim3(256), 0, stream, counters, ranges, big);
     hipLaunchKernelGGL(k_segments_big, dim3(1024), dim3(64 * kBigWaves), 0, stream, sorted, counters, sp, acc, big);
   }
   HIP_TRY(hipGetLastError());
 
+  if (!careful) {
+    // optimistic: K4 straight after K2 (a segment handed to the generic path leaves empty slots); the
+    // final status says whether the generic path was needed
+    if (k4.on) {
+      hipLaunchKernelGGL(k4_fill_ranges, dim3(64), dim3(kThreads), 0, stream, sp, ranges, counters);
+      if (int rc = k4_finish(sp, spare, n_slot, (int64_t)n_sorted, nullptr, nullptr, 0, sorted, spare)) return rc;
+    } else if (sp.packed) {
+      hipLaunchKernelGGL(k_unpack_counts, dim3(grid_for(P, kThreads, 4096)), dim3(kThreads), 0, stream,
+                         acc.row_count, acc.count, P);
+    }
+    HIP_TRY(hipGetLastError());
+    bool redo = false;
+    if (int rc = finish(false, &redo)) return rc;
+    if (redo)  // the generic path was needed: the same call, careful (its accumulators are zeroed again)
+      return bound_impl(ctx, cols, bps, nconf, accps, workspace, workspace_bytes, stream_, sweep, parts, 1);
+    return 0;
+  }
+
   unsigned long long host_ctr[kCtrNDropped + 1];
   HIP_TRY(hipMemcpyAsync(host_ctr, counters, sizeof(host_ctr), hipMemcpyDeviceToHost, stream));
-  HIP_TRY(hipStreamSynchronize(stream));
+  HIP_TRY(host_wait(ctx, stream));
   ctx->stats.kept_rows_in = (int64_t)(host_ctr[kCtrNKept] - host_ctr[kCtrNDropped]);
   n_kept = host_ctr[n_slot];
   for (int i = 0; i < 4; ++i) ctx->stats.sweep_cycles[i] = (int64_t)host_ctr[kCtrSweepCycles + i];
@@ -2988,23 +3202,23 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
   if (host_ctr[kCtrFull]) {
     // Too many overflowing buckets: redo everything on the generic path.
     if (k4.on) {
-      HIP_TRY(hipMemsetAsync(k4rep, 0, (size_t)kK4Rep * kK4MaxPasses * 256 * 4, stream));  // drop K2's records
+      HIP_TRY(zero_async(k4rep, (size_t)kK4Rep * kK4MaxPasses * 256 * 4, stream));  // drop K2's records
       k4_slots = 0;
     } else {
-      HIP_TRY(hipMemsetAsync(acc.row_count, 0, (size_t)P * 8, stream));
-      if (acc.count) HIP_TRY(hipMemsetAsync(acc.count, 0, (size_t)P * 8, stream));
-      if (acc.x) HIP_TRY(hipMemsetAsync(acc.x, 0, (size_t)P * 8, stream));
-      if (acc.y) HIP_TRY(hipMemsetAsync(acc.y, 0, (size_t)P * 8, stream));
+      HIP_TRY(zero_async(acc.row_count, (size_t)P * 8, stream));
+      if (acc.count) HIP_TRY(zero_async(acc.count, (size_t)P * 8, stream));
+      if (acc.x) HIP_TRY(zero_async(acc.x, (size_t)P * 8, stream));
+      if (acc.y) HIP_TRY(zero_async(acc.y, (size_t)P * 8, stream));
     }
     rg = {0ull, host_ctr[n_slot]};
   } else if (host_ctr[kCtrNRanges]) {
     rg.resize(2 * host_ctr[kCtrNRanges]);
     HIP_TRY(hipMemcpyAsync(rg.data(), ranges, rg.size() * 8, hipMemcpyDeviceToHost, stream));
-    HIP_TRY(hipStreamSynchronize(stream));
+    HIP_TRY(host_wait(ctx, stream));
     if (k4.on) {  // the generic path's pairs come in their own array: empty these slots
       const int nr = (int)host_ctr[kCtrNRanges];
       hipLaunchKernelGGL(k4_fill_ranges, dim3((unsigned)std::min(nr, 4096)), dim3(kThreads), 0, stream, sp, ranges,
-                         nr);
+                         counters);
     }
   }
   AsyncFrees k4keep(stream);  // the generic path's pair arrays (until the K4 runs are enqueued)
@@ -3018,24 +3232,20 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
     if (rc) return rc;
     unsigned long long err = 0;
     HIP_TRY(hipMemcpyAsync(&err, counters + kCtrErr, 8, hipMemcpyDeviceToHost, stream));
-    HIP_TRY(hipStreamSynchronize(stream));
+    HIP_TRY(host_wait(ctx, stream));
     if (err) return fail(PDP_ERR_INTERNAL, "radix look-back timed out (generic path)");
   }
   if (k4.on) {
-    if (int rc = k4_finish(sp, spare, k4_slots, kfx, kfy, nkf, sorted, spare)) return rc;
-    unsigned long long kc[kCtrK4Pairs + 1];
-    HIP_TRY(hipMemcpyAsync(kc, counters, sizeof(kc), hipMemcpyDeviceToHost, stream));
-    HIP_TRY(hipStreamSynchronize(stream));
-    ctx->stats.k4_pairs = (int64_t)kc[kCtrK4Pairs];
-    if (kc[kCtrErr] & 4) return fail(PDP_ERR_INTERNAL, "K4 pair histogram disagrees with the pair records");
-    if (kc[kCtrErr] & 2) return fail(PDP_ERR_INTERNAL, "K4 pair records not grouped by partition block");
-    if (kc[kCtrErr]) return fail(PDP_ERR_INTERNAL, "radix look-back timed out (pair passes)");
+    // K2's slots (none when everything went to the generic path: kCtrFull) + the generic path's pairs
+    if (int rc = k4_finish(sp, spare, host_ctr[kCtrFull] ? -1 : n_slot, k4_slots, kfx, kfy, nkf, sorted, spare))
+      return rc;
   } else if (sp.packed) {
     hipLaunchKernelGGL(k_unpack_counts, dim3(grid_for(P, kThreads, 4096)), dim3(kThreads), 0, stream, acc.row_count,
                        acc.count, P);
     HIP_TRY(hipGetLastError());
   }
   }  // configurations
+  if (int rc = finish(true, nullptr)) return rc;
   return 0;
 }
 
@@ -3237,6 +3447,7 @@ int analysis_impl(pdp_ctx* ctx, const int64_t* pid, const int64_t* pk, const dou
   ctx->tile_slot = kCtrTile0;
   ctx->status_at = nullptr;  // first look-back pass of this call clears its status words (next_epoch)
   ctx->stats = pdp_stats{};
+  ctx->cur_debug = ctx->debug;
   const size_t status_bytes = (size_t)L.tiles * kStatusStride * 8;
   const int pkbits = std::max(1, pdp::ceil_log2_u64((uint64_t)P + 1));
   int64_t M = 0;
@@ -3254,14 +3465,14 @@ int analysis_impl(pdp_ctx* ctx, const int64_t* pid, const int64_t* pk, const dou
                                   (uint32_t)P);
       // round 4: the packing is fused into the histogram and the first pass (c5: -0.94 ms of k_ana_pack,
       // +8 B per row in the first pass); PDP_ANA_PACK=1 restores the separate pack
-      const bool fused = ks.passes > 0 && !(ctx->debug & kDebugAnaPack);
+      const bool fused = ks.passes > 0 && !(ctx->cur_debug & kDebugAnaPack);
       if (!fused)
         hipLaunchKernelGGL(k_ana_pack, dim3(g), dim3(kThreads), 0, stream, pid, pk, val, n, U, P, ra, counters);
       if (int rc = sort_recs(ctx, ra, rb, n, ks, hist, off, counters, status, status_bytes, workspace, stream, &sorted,
                              PDP_STAGE_ANALYSIS_SORT, fused ? pid : nullptr, fused ? pk : nullptr,
                              fused ? val : nullptr))
         return rc;
-      if (ctx->debug & kDebugAnaFlags) {  // round-3 form: per-row flags, scan, one thread per group start
+      if (ctx->cur_debug & kDebugAnaFlags) {  // round-3 form: per-row flags, scan, one thread per group start
         hipLaunchKernelGGL(k_ana_group_flags, dim3(g), dim3(kThreads), 0, stream, sorted, n, flags);
         if (int rc = scan_inplace(flags, n, stream)) return rc;
         hipLaunchKernelGGL(k_ana_pairs, dim3(g), dim3(kThreads), 0, stream, sorted, n, flags, num_sampled, ppk, pref,
@@ -3273,7 +3484,7 @@ int analysis_impl(pdp_ctx* ctx, const int64_t* pid, const int64_t* pk, const dou
         if (int rc = scan_inplace(flags, tiles, stream)) return rc;
         // n_partitions of the sampled pairs: bucketed LDS histogram (np_hist) or one atomic per pair
         np_sh = std::max(0, pidbits - 8);
-        np_hist = np_sh <= 14 && !(ctx->debug & kDebugAnaNpartAtomics);
+        np_hist = np_sh <= 14 && !(ctx->cur_debug & kDebugAnaNpartAtomics);
         np_spare = (uint32_t*)(sorted == ra ? rb : ra);
         hipLaunchKernelGGL(k_ana_tile_pairs, dim3((unsigned)tiles), dim3(256), 0, stream, sorted, n, flags, num_sampled,
                            ppk, pref, pcnt, psum, npart, counters, (int)!np_hist);
@@ -3370,7 +3581,7 @@ int analysis_impl(pdp_ctx* ctx, const int64_t* pid, const int64_t* pk, const dou
   if (priv) {
     ProfScope ps_sel(ctx, PDP_STAGE_ANALYSIS_SELECT, stream);
     const int64_t blocks = std::min<int64_t>((P + kAnaSelWaves - 1) / kAnaSelWaves, 16384);
-    if (L.groups.G > 0 && !(ctx->debug & kDebugAnaSelLds)) {
+    if (L.groups.G > 0 && !(ctx->cur_debug & kDebugAnaSelLds)) {
       hipLaunchKernelGGL(k_ana_select_grouped, dim3((unsigned)std::min<int64_t>(P, 65536), cgroups), dim3(64), 0,
                          stream, pref, npart, pbeg, P, cfg_d, nconf, L.groups, (const double*)mom, out->prob_keep);
     } else {  // round-3 form: one launch per regime, lanes = configurations

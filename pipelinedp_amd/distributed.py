@@ -94,6 +94,49 @@ class World:
 
         return move(spid), move(spk), move(sval)
 
+    @staticmethod
+    def key_owner(h, size: int):
+        """Rank owning a privacy-id key hash (int64 tensor): ranks own
+        contiguous ranges of the signed hash order, rank 0 the lowest."""
+        hi = ((h >> 32) & 0xFFFFFFFF) ^ 0x80000000
+        return (hi * size) >> 32
+
+    def exchange_by_key_hash(self, h, pk, value):
+        """Rows of host-encoded input (columnar.encode_rows with a world) ->
+        the rank owning their privacy-id key hash, then dense privacy ids there:
+        the rank's distinct hashes in ascending order, offset by the distinct
+        counts of the lower ranks (one all-gather of one integer).  No key
+        crosses a rank.  The numbering equals one process's
+        (columnar.dense_ids_from_hashes), and rank r receives rank 0's rows for
+        it first, then rank 1's, ...: within a privacy id the concatenated
+        input order is kept, so bounding equals one process over the
+        concatenated input (pipeline_backend.py:476-485).
+        -> (pid, pk, value, num_privacy_ids)."""
+        import torch
+        import torch.distributed as dist
+        dest = self.key_owner(h, self.size)
+        order = torch.argsort(dest, stable=True)
+        counts = torch.bincount(dest, minlength=self.size).to(torch.int64)
+        recv = torch.empty_like(counts)
+        dist.all_to_all_single(recv, counts, group=self.group)
+        in_splits, out_splits = [int(x) for x in counts.tolist()], [int(x) for x in recv.tolist()]
+        total = sum(out_splits)
+
+        def move(t):
+            if t is None:
+                return None
+            out = t.new_empty(total)
+            dist.all_to_all_single(out, t[order].contiguous(), out_splits, in_splits, group=self.group)
+            return out
+
+        hr, pkr, vr = move(h), move(pk), move(value)
+        uniq, inv = torch.unique(hr, sorted=True, return_inverse=True)
+        mine = torch.tensor([uniq.numel()], dtype=torch.int64, device=h.device)
+        every = [torch.empty_like(mine) for _ in range(self.size)]
+        dist.all_gather(every, mine, group=self.group)
+        n_each = [int(x.item()) for x in every]
+        return inv.to(torch.int64) + sum(n_each[:self.rank]), pkr, vr, sum(n_each)
+
     def reduce_scatter_partials(self, parts, num_partitions: int):
         """Sums the ranks' fixed-point partials (int64, exact) and returns the
         owned block's as an executor.Partials of B = padded / size partitions.
@@ -116,18 +159,19 @@ class World:
         return Partials(dst.view(k, b), parts.fields, b)
 
     def aggregate(self, ex, pid, pk, value, num_privacy_ids, num_partitions, bounds, rel, gather=True,
-                  shuffle=False):
+                  shuffle=False, sync=True):
         """Rank-local bound+accumulate, reduce-scatter, owner-side release.
 
         ``shuffle``: first move every row to rank shard_of(pid)
         (``shuffle_by_privacy_id``); without it the rows must already be
-        sharded by privacy id.  Returns (keep [P], metrics [F, P], fields) of
+        sharded by privacy id.  ``sync=False``: the rank-local accumulate does
+        not wait for the stream (check ``ex.status()`` after it drained).  Returns (keep [P], metrics [F, P], fields) of
         ALL partitions on every rank when ``gather`` (all-gather of the owned
         blocks), else of the owned block only."""
         import torch.distributed as dist
         if shuffle and pid is not None:
             pid, pk, value = self.shuffle_by_privacy_id(ex, pid, pk, value)
-        parts = ex.accumulate_partials(pid, pk, value, num_privacy_ids, num_partitions, bounds)
+        parts = ex.accumulate_partials(pid, pk, value, num_privacy_ids, num_partitions, bounds, sync=sync)
         off, length, padded = self.block(num_partitions)
         owned = self.reduce_scatter_partials(parts, num_partitions)
         block_acc = ex.finalize_partials(owned, bounds)

@@ -119,7 +119,8 @@ class DPResult:
                              add_noise=not self._backend._disable_noise, noise_seed=self._backend.noise_seed)
 
     def _inputs(self, torch, device, need_pid, need_value, world=None):
-        """-> pid, pk, value device tensors, U, P, partition keys."""
+        """-> pid, pk, value device tensors, U, P, partition keys, and whether
+        the rows are already sharded by privacy id over the world's ranks."""
         col = self._col
         public = self._public
         multi = world is not None and world.size > 1
@@ -156,12 +157,16 @@ class DPResult:
             value = None
             if need_value:
                 value = torch.as_tensor(col.value).to(device=device, dtype=torch.float64).contiguous()
-            return pid, pk, value, U, P, keys
+            return pid, pk, value, U, P, keys, bool(col.privacy_id_sharded)
         enc = encode_rows(col, self._extractors, public, need_pid=need_pid, need_value=need_value, world=world)
         t = lambda a: torch.from_numpy(a).to(device)  # noqa: E731
-        return (t(enc.pid) if enc.pid is not None else None, t(enc.pk),
-                t(enc.value) if enc.value is not None else None, enc.num_privacy_ids, len(enc.partition_keys),
-                enc.partition_keys)
+        pid, pk, value = (t(enc.pid) if enc.pid is not None else None, t(enc.pk),
+                          t(enc.value) if enc.value is not None else None)
+        U, sharded = enc.num_privacy_ids, False
+        if enc.pid_hash is not None:  # multi-rank host rows: to the owner of their privacy-id key hash
+            pid, pk, value, U = world.exchange_by_key_hash(t(enc.pid_hash), pk, value)
+            sharded = True
+        return pid, pk, value, U, len(enc.partition_keys), enc.partition_keys, sharded
 
     def _compute(self):
         backend = self._backend
@@ -182,7 +187,7 @@ class DPResult:
         need_value = bool(mask & (native.METRIC_SUM | native.METRIC_MEAN | native.METRIC_VARIANCE))
         # A World (also of size 1: the RCCL identity, tests/test_gpu_rccl.py) runs the collective path.
         world = backend.world
-        pid, pk, value, U, P, keys = self._inputs(torch, ex.device, not enforced, need_value, world)
+        pid, pk, value, U, P, keys, presharded = self._inputs(torch, ex.device, not enforced, need_value, world)
         fields = native.metric_fields(mask)
         if world is not None and world.size > 1:
             # every rank must take the same branch below (a rank with P == 0 alone would leave the others
@@ -191,8 +196,8 @@ class DPResult:
         if P == 0:  # e.g. public_partitions=[]: nothing to release (reference: empty collection)
             return keys, np.zeros(0, dtype=bool), fields, np.zeros((len(fields), 0))
         if world is not None:
-            presharded = isinstance(self._col, ColumnarData) and self._col.privacy_id_sharded
-            keep, out, fields = world.aggregate(ex, pid, pk, value, U, P, bounds, rel, shuffle=not presharded)
+            keep, out, fields = world.aggregate(ex, pid, pk, value, U, P, bounds, rel,
+                                                shuffle=not presharded and pid is not None)
         else:
             acc = ex.accumulate(pid, pk, value, U, P, bounds)
             keep, out, fields = ex.release(acc, rel, bounds)

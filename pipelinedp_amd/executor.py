@@ -151,7 +151,7 @@ class HipExecutor:
                               int(num_partitions))
 
     @staticmethod
-    def _bound_params(cfg: BoundConfig):
+    def _bound_params(cfg: BoundConfig, flags: int = 0):
         seed = cfg.sampling_seed if cfg.sampling_seed is not None else secrets.randbits(64)
         return native.BoundParams(
             cfg.metrics_mask, int(cfg.bounds_already_enforced), cfg.max_partitions_contributed,
@@ -159,13 +159,15 @@ class HipExecutor:
             int(cfg.min_sum_per_partition is not None),
             float(cfg.min_value or 0.0), float(cfg.max_value or 0.0),
             float(cfg.min_sum_per_partition or 0.0), float(cfg.max_sum_per_partition or 0.0),
-            seed, int(cfg.debug_force_fallback), int(cfg.debug_flags))
+            seed, int(cfg.debug_force_fallback), int(cfg.debug_flags), int(flags), 0)
 
     def accumulate(self, pid, pk, value, num_privacy_ids: int, num_partitions: int, cfg: BoundConfig,
-                   acc: Optional[Accumulators] = None) -> Accumulators:
-        """pdp_bound_accumulate on int64 pid/pk and float64 value device tensors."""
+                   acc: Optional[Accumulators] = None, sync: bool = True) -> Accumulators:
+        """pdp_bound_accumulate on int64 pid/pk and float64 value device tensors.
+        sync=False (PDP_BOUND_ASYNC): only enqueues work on the current stream
+        (hipGraph-capturable); check status() once the stream has drained."""
         cols = self._columns(pid, pk, value, num_privacy_ids, num_partitions)
-        bp = self._bound_params(cfg)
+        bp = self._bound_params(cfg, 0 if sync else native.BOUND_ASYNC)
         if acc is None:
             acc = Accumulators(self.torch, num_partitions, self.device, cfg.metrics_mask)
         nbytes = ctypes.c_size_t(0)
@@ -179,11 +181,11 @@ class HipExecutor:
         return acc
 
     def accumulate_partials(self, pid, pk, value, num_privacy_ids: int, num_partitions: int,
-                            cfg: BoundConfig) -> Partials:
+                            cfg: BoundConfig, sync: bool = True) -> Partials:
         """pdp_bound_accumulate_partials: the rank-local accumulate of the
         multi-GPU path, sums in exported fixed point (see Partials)."""
         cols = self._columns(pid, pk, value, num_privacy_ids, num_partitions)
-        bp = self._bound_params(cfg)
+        bp = self._bound_params(cfg, 0 if sync else native.BOUND_ASYNC)
         fields = Partials.fields_for(cfg.metrics_mask)
         P = max(int(num_partitions), 1)
         parts = Partials(self.torch.empty((len(fields), P), dtype=self.torch.int64, device=self.device), fields,
@@ -382,6 +384,13 @@ class HipExecutor:
         cnt = (ctypes.c_int64 * n)()
         native.check(self.lib.pdp_profile_read(self.ctx, ms, cnt, int(reset)), "pdp_profile_read")
         return {s: (ms[i], cnt[i]) for i, s in enumerate(native.STAGES)}
+
+    def status(self) -> int:
+        """pdp_get_status: 0, or the PDP_ERR_* code of the last accumulate(sync=False)
+        (native.ERR_NEEDS_SYNC: redo it with sync=True).  Call after the stream drained."""
+        st = ctypes.c_int32(0)
+        native.check(self.lib.pdp_get_status(self.ctx, ctypes.byref(st)), "pdp_get_status")
+        return int(st.value)
 
     def stats(self) -> native.Stats:
         s = native.Stats()

@@ -11,6 +11,9 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("PDP_HIP_LIB") or os.path.join(_HERE, "libpdp_hip.so")  # env: experiment builds
 
 PDP_OK = 0
+ERR_OUT_OF_RANGE, ERR_INTERNAL, ERR_NEEDS_SYNC = -4, -5, -6
+BOUND_ASYNC = 1  # pdp_bound_params.flags: no host synchronisation (pdp_get_status afterwards)
+ABI_VERSION = 2
 METRIC_COUNT, METRIC_SUM, METRIC_MEAN, METRIC_VARIANCE, METRIC_PRIVACY_ID_COUNT = 1, 2, 4, 8, 16
 FIELD_NAMES = {0: "variance", 1: "mean", 2: "count", 3: "sum", 4: "privacy_id_count"}
 NOISE_LAPLACE, NOISE_GAUSSIAN = 0, 1
@@ -29,7 +32,7 @@ DEBUG_ANA_NPART_ATOMICS = 32
 DEBUG_ANA_PACK = 64
 DEBUG_ANA_FLAGS = 128
 DEBUG_ANA_SEL_LDS = 256
-DEBUG_K4_TILESCAN = 1024
+DEBUG_DEV_OCC3 = 512
 
 c_i32, c_i64, c_u64, c_f64 = ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64, ctypes.c_double
 c_vp = ctypes.c_void_p
@@ -46,7 +49,8 @@ class BoundParams(ctypes.Structure):
                 ("has_value_bounds", c_i32), ("has_partition_bounds", c_i32),
                 ("min_value", c_f64), ("max_value", c_f64),
                 ("min_sum_per_partition", c_f64), ("max_sum_per_partition", c_f64),
-                ("sampling_seed", c_u64), ("debug_force_fallback", c_i32), ("reserved", c_i32)]
+                ("sampling_seed", c_u64), ("debug_force_fallback", c_i32), ("reserved", c_i32),
+                ("flags", c_i32), ("reserved2", c_i32)]
 
 
 class Accumulators(ctypes.Structure):
@@ -100,7 +104,7 @@ class Stats(ctypes.Structure):
     _fields_ = [("kept_rows_in", c_i64), ("fallback_rows", c_i64), ("fallback_ranges", c_i64),
                 ("sort_passes", c_i32), ("bucket_low_bits", c_i32), ("sweep_cycles", c_i64 * 4),
                 ("sweep_tiles", c_i64), ("filter_rows", c_i64), ("k4_slots", c_i64), ("k4_pairs", c_i64),
-                ("k4_passes", c_i32), ("reserved_", c_i32)]
+                ("k4_passes", c_i32), ("host_waits", c_i32)]
 
 
 # Every symbol declared in include/pdp_hip.h: (name, restype, argtypes).
@@ -148,6 +152,7 @@ SIGNATURES = [
     ("pdp_stream_copy", c_i32, [c_vp, c_vp, c_i64, c_vp]),
     ("pdp_fp64_probe", c_i32, [ctypes.POINTER(c_f64), c_vp]),
     ("pdp_get_stats", c_i32, [c_vp, ctypes.POINTER(Stats)]),
+    ("pdp_get_status", c_i32, [c_vp, ctypes.POINTER(c_i32)]),
     ("pdp_profile_enable", c_i32, [c_vp, c_i32]),
     ("pdp_profile_read", c_i32, [c_vp, ctypes.POINTER(c_f64), ctypes.POINTER(c_i64), c_i32]),
 ]

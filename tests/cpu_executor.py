@@ -46,7 +46,7 @@ class CpuExecutor:
         self.device = torch.device("cpu")
         self.calls = []
 
-    def accumulate(self, pid, pk, value, num_privacy_ids, num_partitions, cfg):
+    def accumulate(self, pid, pk, value, num_privacy_ids, num_partitions, cfg, acc=None, sync=True):
         self.calls.append(("accumulate", int(pk.numel())))
         acc = o.bound_and_accumulate(None if pid is None else pid.numpy(), pk.numpy(),
                                      None if value is None else value.numpy(), num_partitions, _bound_params(cfg),
@@ -63,7 +63,7 @@ class CpuExecutor:
             acc.nsumsq = y
         return _Acc(self.torch, acc, cfg.metrics_mask, num_partitions)
 
-    def accumulate_partials(self, pid, pk, value, num_privacy_ids, num_partitions, cfg):
+    def accumulate_partials(self, pid, pk, value, num_privacy_ids, num_partitions, cfg, sync=True):
         """pdp_bound_accumulate_partials restated: the oracle's kept pairs in
         K4's exported fixed point (pdp_oracle.k4_partials)."""
         from pipelinedp_amd.executor import Partials

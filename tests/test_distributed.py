@@ -48,7 +48,7 @@ class OracleExecutor:
     signatures, computed by the CPU oracle on torch CPU tensors (test
     infrastructure only)."""
 
-    def accumulate_partials(self, pid, pk, value, num_privacy_ids, num_partitions, bounds):
+    def accumulate_partials(self, pid, pk, value, num_privacy_ids, num_partitions, bounds, sync=True):
         import torch
 
         from pipelinedp_amd.executor import Partials
@@ -164,13 +164,13 @@ def test_two_ranks_match_single_process(two_rank_run):
 
 # --- DPEngine.aggregate with a 2-rank world (gloo) ---------------------------
 # Rows are dealt round-robin (NOT sharded by privacy id) and carry string keys,
-# so the run exercises the cross-rank key dictionaries (columnar._global_keys),
-# the num_partitions agreement, the privacy-id shuffle (World.shuffle_by_privacy_id
-# over all_to_all_single), reduce-scatter and owner-side release.  The HIP
-# executor is replaced by tests/cpu_executor.py (oracle on CPU tensors).
-# Expected: one process over the concatenation [rank 0 rows, rank 1 rows] --
-# the same dense ids, the same privacy-id row order, hence identical sampling
-# and Philox draws: counts / keep decisions exact, fp64 to 1e-9.
+# so the run exercises the cross-rank partition dictionary (columnar._global_keys),
+# the num_partitions agreement, the privacy-id exchange by key hash
+# (World.exchange_by_key_hash over all_to_all_single; dense ids numbered by the
+# owner), reduce-scatter and owner-side release.  The HIP executor is replaced
+# by tests/cpu_executor.py (oracle on CPU tensors).  Expected: one process over
+# the concatenation [rank 0 rows, rank 1 rows] -- the same dense ids, the same
+# privacy-id row order, hence identical sampling and Philox draws: bit for bit.
 
 
 def _engine_rows():
@@ -261,3 +261,59 @@ def _disagree_worker(rank, world_size, port, outdir):
             open(os.path.join(outdir, f"raised{rank}"), "w").close()
     finally:
         dist.destroy_process_group()
+
+
+# --- scalable host encoding: 1e5 distinct privacy ids over 2 ranks -----------
+# No privacy-id key crosses a rank: the rows carry their key hashes and
+# World.exchange_by_key_hash moves them to the hash owner, which numbers them;
+# only the partition dictionary is all-gathered.  Bitwise equal to one process.
+
+
+def _many_user_rows():
+    pid, pk, val = o.synth_rows(200_000, 100_000, 50, seed=29, zipf_s=1.1)
+    return [(f"user{a}", f"movie{b}", float(v)) for a, b, v in zip(pid, pk, val)]
+
+
+def _many_users_worker(rank, world_size, port, outdir):
+    import json
+
+    import torch.distributed as dist
+
+    from pipelinedp_amd.distributed import World
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world_size)
+    gathered = []
+    real = dist.all_gather_object
+
+    def spy(out, obj, group=None):
+        gathered.append(len(obj) if hasattr(obj, "__len__") else 1)
+        return real(out, obj, group=group)
+
+    dist.all_gather_object = spy
+    try:
+        rows = _many_user_rows()[rank::world_size]
+        out, calls = _run_engine(rows, World(rank, world_size))
+        with open(os.path.join(outdir, f"many{rank}.json"), "w") as f:
+            json.dump({"out": out, "calls": calls, "gathered": gathered}, f)
+    finally:
+        dist.all_gather_object = real
+        dist.destroy_process_group()
+
+
+def test_many_privacy_ids_two_ranks_no_key_exchange_bitwise(tmp_path):
+    import json
+
+    import torch.multiprocessing as mp
+    mp.spawn(_many_users_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    runs = [json.load(open(os.path.join(tmp_path, f"many{r}.json"))) for r in range(2)]
+    rows = _many_user_rows()
+    want, _ = _run_engine(rows[0::2] + rows[1::2], None)
+    assert len(want) > 20
+    for r in runs:
+        # one all_gather_object per rank: the partition keys (<= 50), never the 1e5 privacy-id keys
+        assert len(r["gathered"]) == 1 and r["gathered"][0] <= 50, r["gathered"]
+        got = [(k, tuple(v)) for k, v in r["out"]]
+        assert [k for k, _ in got] == [k for k, _ in want]
+        for (_, g), (_, w) in zip(got, want):
+            np.testing.assert_array_equal(g, w)
+    acc_rows = [c[1] for r in runs for c in r["calls"] if c[0] == "accumulate"]
+    assert sum(acc_rows) == len(rows)

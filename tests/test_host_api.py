@@ -158,7 +158,14 @@ def test_host_encoding():
     ex = pdp.DataExtractors(lambda r: r[0], lambda r: r[1], lambda r: r[2])
     e = encode_rows(rows, ex)
     assert e.partition_keys == ["a", "b", "c"] and e.pk.tolist() == [0, 1, 2, 0]
-    assert e.pid.tolist() == [0, 1, 0, 2] and e.num_privacy_ids == 3
+    # privacy ids numbered by the ascending order of their key hash (columnar.dense_ids_from_hashes)
+    from pipelinedp_amd.columnar import key_hashes
+    h = key_hashes(["u1", "u2", "u3"])
+    rank = {k: int(r) for k, r in zip(["u1", "u2", "u3"], np.argsort(np.argsort(h)))}
+    assert e.pid.tolist() == [rank["u1"], rank["u2"], rank["u1"], rank["u3"]] and e.num_privacy_ids == 3
+    # the hash is process-independent (blake2b of canonical bytes; numpy scalars / integral floats as ints)
+    assert key_hashes([5])[0] == key_hashes([np.int64(5)])[0] == key_hashes([5.0])[0]
+    assert len(set(key_hashes(["5", 5, (5,), b"5", None, 5.5]).tolist())) == 6
     e = encode_rows(rows, ex, public_partitions=["c", "zz", "a", "c"])
     assert e.partition_keys == ["c", "zz", "a"] and e.pk.tolist() == [2, -1, 0, 2]
     np.testing.assert_array_equal(e.value, [1, 2, 3, 4])

@@ -29,7 +29,7 @@ def test_library_exports_every_declared_symbol():
         assert hasattr(lib, s), s
     bound = {name for name, _, _ in native.SIGNATURES}
     assert set(syms) == bound, set(syms) ^ bound
-    assert lib.pdp_abi_version() == 1
+    assert lib.pdp_abi_version() == native.ABI_VERSION
 
 
 def test_gaussian_sigma_known_answers():
