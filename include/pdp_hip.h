@@ -208,7 +208,7 @@ int pdp_bound_accumulate(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_
  * in [0, 2^32) per rank.  nan[p] counts NaN terms: + 1 per x NaN, + 2^32 per
  * y NaN.  Arrays are [num_partitions] int64; row_count / count / x_* / y_* /
  * nan as the metrics need them (x: SUM / MEAN / VARIANCE, y: VARIANCE, nan:
- * with x).  Needs the K4 reduction (num_rows < 2^32). */
+ * with x).  Any row count (with >= 2^32 rows: L_inf < 131072). */
 typedef struct pdp_partials {
   int64_t* row_count;
   int64_t* count;

@@ -82,7 +82,8 @@ enum Counter {
   kCtrK4In = 16,      // K4: records in the first pair pass's input (slots + generic-path pairs)
   kCtrK4Pairs = 17,   // K4: (pid, pk) pair records (non-empty slots)
   kCtrK4Chunk = 18,   // K4: pair records per reduce chunk (k4_total: ~1024 chunks, 4096 .. kK4Chunk)
-  kCtrTile0 = 19,  // 19..63 tile claim counters, one per onesweep launch
+  kCtrK4Slots = 19,   // K4: compacted pair records written by K2 (SegParams.k4ctr)
+  kCtrTile0 = 20,  // 20..63 tile claim counters, one per onesweep launch
 };
 
 struct __align__(16) Rec {
@@ -209,6 +210,9 @@ struct SegParams {
   // k4soa bytes further (k4_soa_offset), so the first pair pass reads 4 bytes of an empty slot, not 12
   int64_t k4soa;
   unsigned int* k4hist;  // [kK4Rep][kK4MaxPasses][256]
+  // != null: compacted pair records -- K2 writes only its kept groups, at slots claimed from this
+  // counter (k4_claim, one atomic per wave), no empty records; null: the slot form above
+  unsigned long long* k4ctr;
   int k4sh;              // partition block = pk >> k4sh
   int k4passes;
   int k4shift[3];
@@ -232,7 +236,7 @@ constexpr int kDebugWalkOnly = 2097152;  // k_lean loads rows and finds segments
 constexpr int kDebugNoLinf = 8388608;     // k_lean skips the L_inf ranking (timing ablation, results invalid)
 constexpr int kDebugNoSums = 16777216;    // k_lean skips the kept-row sums (timing ablation, results invalid)
 constexpr int kDebugForceHotCache = 33554432;  // k_lean uses the LDS partition cache at any L0
-constexpr int kDebugFewBlocks = 67108864;      // k_lean grid of 4096 blocks (longer grid-stride per block)
+constexpr int kDebugThin2 = 67108864;          // K4 on: the LDS-staged k_thin2 instead of k_thin (round 5 experiment)
 constexpr int kDebugNoFilter = 134217728;      // never use the L0 pre-filter (pdp_filter.inc)
 constexpr int kDebugForceFilter = 268435456;   // use the L0 pre-filter whenever it applies (small inputs too)
 constexpr int kDebugNoThin = 536870912;        // bound the pre-filter's survivors with k_lean instead of k_thin
@@ -251,7 +255,7 @@ constexpr int kDebugAnaPack = 64;           // utility analysis: separate pack k
 constexpr int kDebugAnaFlags = 128;         // utility analysis: round-3 per-row flags + scan pair extraction
 constexpr int kDebugAnaSelLds = 256;        // utility analysis: round-3 per-regime selection kernels
 constexpr int kDebugDevOcc3 = 512;          // device-sized look-back passes at 3 blocks per CU (spills)
-constexpr int kDebugK4TileScan = 1024;      // K4 pair passes by reduce-then-scan (unused since round 5)
+constexpr int kDebugK4Compact = 1024;       // K2 writes compacted K4 pair records (k4_claim) instead of a slot per row
 // Timing ablations whose results are invalid: accepted only by a -DPDP_DEBUG_BUILD library.
 constexpr int kAblationFlags = kDebugSortOnly | kDebugNoLookback | kDebugLinearWrite | kDebugNoScatter |
                                kDebugNoAtomics | kDebugWalkOnly | kDebugNoLinf | kDebugNoSums | kDebugFilterTiming;
@@ -2380,7 +2384,7 @@ double noise_scale(int kind, double eps, double delta, double l0, double linf) {
   return pdp_gaussian_sigma(eps, delta, std::sqrt(l0) * linf);
 }
 
-bool k4_enabled(int64_t n, bool sweep, int debug = 0);
+bool k4_enabled(int64_t n, bool sweep, int debug = 0, int64_t linf = 1);
 int decode_status(pdp_ctx* ctx, const unsigned long long* h);
 
 }  // namespace
@@ -2587,7 +2591,7 @@ FilterPlan filter_plan(int64_t n, int64_t U, const pdp_bound_params* bp, int deb
 }
 
 // K4 plan (pdp_reduce.inc): partition-block digits of the pair passes and the
-// fixed-point scales.  Off for the parameter sweep, for >= 2^32 rows (the
+// fixed-point scales.  Off for the parameter sweep (and with debug flag NO_K4; the
 // packed per-block counts) and with PDP_K4=0 (A/B experiments): the
 // accumulators then take fp64 atomics, as in round 2.
 struct K4Plan {
@@ -2609,13 +2613,19 @@ int k4_exponent(double M) {
   return std::max(-1000, std::min(1000, 62 - e));
 }
 
-bool k4_enabled(int64_t n, bool sweep, int debug) {
-  return !sweep && n < (1ll << 32) && !(debug & kDebugNoK4);
+// Any row count (round 5; round 4 fell back to fp64 atomics at >= 2^32 rows).  What bounds K4 is per
+// reduce chunk (<= kK4Chunk pair records): a partition's (count << 32 | pairs) LDS word needs the
+// chunk's kept rows of one partition < 2^32, i.e. L_inf < 2^32 / kK4Chunk when rows >= 2^32 (below 2^32
+// rows the whole input is smaller); the fixed-point (lo, hi) sums hold <= 2^32 pairs per partition (U <=
+// 2^32, one pair per privacy id) exactly.
+bool k4_enabled(int64_t n, bool sweep, int debug, int64_t linf) {
+  if (sweep || (debug & kDebugNoK4)) return false;
+  return n < (1ll << 32) || linf < (1ll << 32) / kK4Chunk;
 }
 
 K4Plan k4_plan(const pdp_bound_params* bp, const SegParams& sp, int64_t n, int64_t P, bool sweep) {
   K4Plan k{};
-  k.on = k4_enabled(n, sweep, sp.debug);
+  k.on = k4_enabled(n, sweep, sp.debug, bp->max_contributions_per_partition);
   if (!k.on) return k;
   const int pkb = std::max(1, pdp::ceil_log2_u64((uint64_t)std::max<int64_t>(P, 1)));
   // the 2048-partition window (56 KiB of LDS: 2 reduce workgroups per CU) unless the 4096 one saves a pass
@@ -2649,7 +2659,7 @@ K4Plan k4_plan(const pdp_bound_params* bp, const SegParams& sp, int64_t n, int64
   // split slots (PDP_K4_SOA=1; parity-green): look-back passes only (k_pair_tile_counts reads 12-byte
   // slots).  Off: c4 pair passes 8.40 / 8.63 ms against 8.35 / 8.34 with 12-byte slots, c3 0.65 against
   // 0.62 (the values wait for their keys), for 1 % fewer pair-pass bytes (r04z7)
-  k.soa = k.p12 && (sp.debug & kDebugK4Soa) && !(sp.debug & kDebugK4TileScan);
+  k.soa = k.p12 && (sp.debug & kDebugK4Soa);
   return k;
 }
 
@@ -2865,7 +2875,9 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
   const K4Plan k4 = k4_plan(bp, sp, n, P, sweep);
   ctx->last_k4 = k4.on;
   ctx->last_filter = false;
-  if (parts && !k4.on) return fail(PDP_ERR_INVALID_ARG, "partials need the K4 reduction (num_rows < 2^32, PDP_K4 on)");
+  if (parts && !k4.on)
+    return fail(PDP_ERR_INVALID_ARG, "partials need the K4 reduction (not with debug flag NO_K4, nor with >= 2^32 "
+                                     "rows and L_inf >= 131072)");
   const Layout L = layout_for(n, sweep, k4.on ? P : 0, sp.want_y != 0);
   if (!workspace || workspace_bytes < L.total) return fail(PDP_ERR_WORKSPACE, "workspace too small");
   char* ws = (char*)workspace;
@@ -2904,9 +2916,13 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
   unsigned long long* k4hi = k4lo + P;
   unsigned int* k4fl = (unsigned int*)(k4hi + P);
   Rec* k4y = sp.want_y ? (Rec*)(ws + L.recs_c) : nullptr;
-  auto k4_attach = [&](SegParams& q, Rec* slots) {
+  // compacted pair records from K2 (round 5): only the kept groups reach K4's first pair pass
+  // (c3: 40M records instead of 67.7M slots); debug flag K4_SLOT_FORM restores the slot form
+  bool k4_compact = false;  // per configuration, with the K2 kernel (below)
+  auto k4_attach = [&](SegParams& q, Rec* slots, bool compact) {
     if (!k4.on) return;
     q.packed = 0;
+    q.k4ctr = compact ? counters + kCtrK4Slots : nullptr;
     q.k4x = slots;
     q.k4y = k4y;
     q.k4hist = k4rep;
@@ -2951,7 +2967,7 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
   if (k4.on) HIP_TRY(zero_async(k4rep, (size_t)kK4Rep * kK4MaxPasses * 256 * 4, stream));
 
   if (bp->bounds_already_enforced) {
-    k4_attach(sp, recs_a);
+    k4_attach(sp, recs_a, false);  // row i -> slot i
     {
       ProfScope ps(ctx, PDP_STAGE_ENFORCED, stream);
       hipLaunchKernelGGL(k_enforced, dim3(grid_for(n, kThreads, 8192)), dim3(kThreads), 0, stream, cols->pk,
@@ -3112,7 +3128,16 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
   sp = sps[c];
   acc = accs[c];
   sp.packed = !k4.on && sp.want_count && n < (1ll << 32);
-  k4_attach(sp, spare);
+  const bool thin = fpl.on && bp->max_partitions_contributed <= kThinMaxL0 &&
+                    bp->max_contributions_per_partition <= kThinMaxLinf &&
+                    !(sp.debug & (kDebugBatchKernel | kDebugNoThin));
+  // debug flag THIN2: the LDS-staged k_thin2 (round 5 experiment, slower: DESIGN.md 3.2)
+  const bool thin2 = thin && k4.on && (sp.debug & kDebugThin2);
+  // debug flag K4_COMPACT: K2 claims compacted pair slots (k4_claim) instead of writing a slot per row
+  // with empties.  Measured slower: the claims are atomics on ONE counter, which serialise (r05f: c3
+  // k_thin2 +1.3 ms for a 0.26 ms shorter first pair pass; c4 k_lean 8.56 -> 150 ms).
+  k4_compact = k4.on && (sp.debug & kDebugK4Compact);
+  k4_attach(sp, spare, k4_compact);
   if (c > 0) {
     // fresh K2/KF counters; the kept-row count of the shared sort stays
     unsigned long long reset[kCtrSweepCycles] = {};
@@ -3122,18 +3147,20 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
   }
   {
     ProfScope ps(ctx, PDP_STAGE_BUCKETS, stream);
-    const bool thin = fpl.on && bp->max_partitions_contributed <= kThinMaxL0 &&
-                      bp->max_contributions_per_partition <= kThinMaxLinf &&
-                      !(sp.debug & (kDebugBatchKernel | kDebugNoThin));
     if (thin) {
-      const int64_t waves = ((int64_t)n_sorted + kThinChunk - 1) / kThinChunk;
+      const bool v2 = thin2;
+      const int64_t chunk = v2 ? kThin2Chunk : kThinChunk;
+      const int64_t waves = ((int64_t)n_sorted + chunk - 1) / chunk;
       // LDS partition cache on: the Zipf-head pairs' HBM atomics otherwise dominate (c3: K2 8.1 -> 3.4 ms);
       // K4 writes pair records instead of atomics, no cache
       const bool tcache = !k4.on;
       const int64_t blocks =
           std::max<int64_t>(1, std::min<int64_t>((waves + 3) / 4, (sp.debug & kDebugOddGrid) ? 7 : 8192));
       const int64_t l0 = bp->max_partitions_contributed;
-      auto kern = l0 <= 1 ? (tcache ? k_thin<true, 1> : k_thin<false, 1>)
+      auto kern = v2 ? (l0 <= 1 ? k_thin2<1> : l0 <= 2 ? k_thin2<2> : l0 <= 4 ? k_thin2<4> : k_thin2<8>)
+                : k4_compact ? (l0 <= 1 ? k_thin<false, 1, true> : l0 <= 2 ? k_thin<false, 2, true>
+                                : l0 <= 4 ? k_thin<false, 4, true> : k_thin<false, 8, true>)
+                : l0 <= 1 ? (tcache ? k_thin<true, 1> : k_thin<false, 1>)
                 : l0 <= 2 ? (tcache ? k_thin<true, 2> : k_thin<false, 2>)
                 : l0 <= 4 ? (tcache ? k_thin<true, 4> : k_thin<false, 4>)
                           : (tcache ? k_thin<true, 8> : k_thin<false, 8>);
@@ -3141,7 +3168,7 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
                          (int)bp->debug_force_fallback);
     } else if (bp->max_partitions_contributed <= kLeanMaxL0 && !(sp.debug & kDebugBatchKernel)) {
       const int64_t waves = ((int64_t)n_sorted + kLeanChunk - 1) / kLeanChunk;
-      int64_t max_blocks = (sp.debug & kDebugFewBlocks) ? 4096 : kLeanMaxBlocks;
+      int64_t max_blocks = kLeanMaxBlocks;
       if (sp.debug & kDebugOddGrid) max_blocks = 5;
       const int64_t blocks = std::max<int64_t>(1, (waves + 3) / 4 < max_blocks ? (waves + 3) / 4 : max_blocks);
       const bool sorted_l0 = bp->max_partitions_contributed >= kSortMinL0 && !(sp.debug & kDebugLeanMinSearch);
@@ -3174,8 +3201,10 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
     // optimistic: K4 straight after K2 (a segment handed to the generic path leaves empty slots); the
     // final status says whether the generic path was needed
     if (k4.on) {
-      hipLaunchKernelGGL(k4_fill_ranges, dim3(64), dim3(kThreads), 0, stream, sp, ranges, counters);
-      if (int rc = k4_finish(sp, spare, n_slot, (int64_t)n_sorted, nullptr, nullptr, 0, sorted, spare)) return rc;
+      if (!k4_compact) hipLaunchKernelGGL(k4_fill_ranges, dim3(64), dim3(kThreads), 0, stream, sp, ranges, counters);
+      if (int rc = k4_finish(sp, spare, k4_compact ? (int)kCtrK4Slots : n_slot, (int64_t)n_sorted, nullptr, nullptr, 0,
+                             sorted, spare))
+        return rc;
     } else if (sp.packed) {
       hipLaunchKernelGGL(k_unpack_counts, dim3(grid_for(P, kThreads, 4096)), dim3(kThreads), 0, stream,
                          acc.row_count, acc.count, P);
@@ -3215,7 +3244,7 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
     rg.resize(2 * host_ctr[kCtrNRanges]);
     HIP_TRY(hipMemcpyAsync(rg.data(), ranges, rg.size() * 8, hipMemcpyDeviceToHost, stream));
     HIP_TRY(host_wait(ctx, stream));
-    if (k4.on) {  // the generic path's pairs come in their own array: empty these slots
+    if (k4.on && !k4_compact) {  // the generic path's pairs come in their own array: empty these slots
       const int nr = (int)host_ctr[kCtrNRanges];
       hipLaunchKernelGGL(k4_fill_ranges, dim3((unsigned)std::min(nr, 4096)), dim3(kThreads), 0, stream, sp, ranges,
                          counters);
@@ -3227,6 +3256,7 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
   if (!rg.empty()) {
     SegParams gsp = sp;
     if (k4.on) gsp.k4hist = k4rep;  // replica 0: global atomics from the generic path
+    gsp.k4ctr = nullptr;            // KF writes one slot per group of its own array
     int rc = run_generic(ctx, sorted, spare, alt, rg, plan, gsp, bp, ks.num_pids, ks.num_parts, acc, hist, off,
                          counters, status, status_bytes, workspace, stream, &k4keep, &kfx, &kfy, &nkf);
     if (rc) return rc;
@@ -3237,7 +3267,8 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
   }
   if (k4.on) {
     // K2's slots (none when everything went to the generic path: kCtrFull) + the generic path's pairs
-    if (int rc = k4_finish(sp, spare, host_ctr[kCtrFull] ? -1 : n_slot, k4_slots, kfx, kfy, nkf, sorted, spare))
+    if (int rc = k4_finish(sp, spare, host_ctr[kCtrFull] ? -1 : k4_compact ? (int)kCtrK4Slots : n_slot, k4_slots, kfx,
+                           kfy, nkf, sorted, spare))
       return rc;
   } else if (sp.packed) {
     hipLaunchKernelGGL(k_unpack_counts, dim3(grid_for(P, kThreads, 4096)), dim3(kThreads), 0, stream, acc.row_count,
@@ -3626,7 +3657,7 @@ int pdp_finalize_partials(pdp_ctx* ctx, const pdp_partials* parts, int64_t P, co
     HIP_TRY(hipMemcpyAsync(acc->row_count, parts->row_count, (size_t)P * 8, hipMemcpyDeviceToDevice, stream));
   if (sp.want_count && acc->count != parts->count)
     HIP_TRY(hipMemcpyAsync(acc->count, parts->count, (size_t)P * 8, hipMemcpyDeviceToDevice, stream));
-  // the exponents K4 used: k4_plan depends on the bounds and metrics only (n < 2^32 for partials)
+  // the exponents K4 used: k4_plan depends on the bounds and metrics only
   const K4Plan k4 = k4_plan(bp, sp, 1, std::max<int64_t>(P, 1), false);
   if (!k4.on) return fail(PDP_ERR_INVALID_ARG, "partials need the K4 reduction (PDP_K4 on)");
   const unsigned grid = (unsigned)grid_for(P, kThreads, 4096);

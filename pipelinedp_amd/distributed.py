@@ -140,23 +140,26 @@ class World:
     def reduce_scatter_partials(self, parts, num_partitions: int):
         """Sums the ranks' fixed-point partials (int64, exact) and returns the
         owned block's as an executor.Partials of B = padded / size partitions.
-        One collective for all arrays: the [K, padded] partials are laid out
-        as [size, K, B] so that reduce_scatter_tensor hands rank r its
-        [K, B] slice."""
+        Each field's row is already rank-major (rank r owns columns
+        [r*B, (r+1)*B)), so one reduce_scatter_tensor per field (K <= 7) runs
+        on the row in place: no re-layout copy.  Partials allocated with
+        ``padded`` columns (aggregate does) need no padding copy either."""
         import torch
         import torch.distributed as dist
 
         from .executor import Partials
         _, _, padded = self.block(num_partitions)
         b = padded // self.size
-        data = parts.data[:, :num_partitions]
+        data = parts.data
         k = data.shape[0]
-        if padded != num_partitions:
-            data = torch.cat([data, data.new_zeros((k, padded - num_partitions))], dim=1)
-        src = data.reshape(k, self.size, b).permute(1, 0, 2).reshape(-1)  # [size * K * B], rank-major
-        dst = src.new_empty(k * b)
-        dist.reduce_scatter_tensor(dst, src, op=dist.ReduceOp.SUM, group=self.group)
-        return Partials(dst.view(k, b), parts.fields, b)
+        if data.shape[1] < padded:
+            data = torch.cat([data[:, :num_partitions], data.new_zeros((k, padded - num_partitions))], dim=1)
+        elif data.shape[1] > num_partitions:
+            data[:, num_partitions:padded].zero_()  # padding columns sum to zero
+        dst = data.new_empty((k, b))
+        for i in range(k):
+            dist.reduce_scatter_tensor(dst[i], data[i, :padded], op=dist.ReduceOp.SUM, group=self.group)
+        return Partials(dst, parts.fields, b)
 
     def aggregate(self, ex, pid, pk, value, num_privacy_ids, num_partitions, bounds, rel, gather=True,
                   shuffle=False, sync=True):
@@ -171,8 +174,9 @@ class World:
         import torch.distributed as dist
         if shuffle and pid is not None:
             pid, pk, value = self.shuffle_by_privacy_id(ex, pid, pk, value)
-        parts = ex.accumulate_partials(pid, pk, value, num_privacy_ids, num_partitions, bounds, sync=sync)
         off, length, padded = self.block(num_partitions)
+        parts = ex.accumulate_partials(pid, pk, value, num_privacy_ids, num_partitions, bounds, sync=sync,
+                                       padded=padded)
         owned = self.reduce_scatter_partials(parts, num_partitions)
         block_acc = ex.finalize_partials(owned, bounds)
         keep, out, fields = ex.release(block_acc, rel, bounds, pk_offset=off, num_partitions=padded // self.size)

@@ -181,15 +181,20 @@ class HipExecutor:
         return acc
 
     def accumulate_partials(self, pid, pk, value, num_privacy_ids: int, num_partitions: int,
-                            cfg: BoundConfig, sync: bool = True) -> Partials:
+                            cfg: BoundConfig, sync: bool = True, padded: Optional[int] = None) -> Partials:
         """pdp_bound_accumulate_partials: the rank-local accumulate of the
-        multi-GPU path, sums in exported fixed point (see Partials)."""
+        multi-GPU path, sums in exported fixed point (see Partials).
+        ``padded``: allocate that many columns (>= num_partitions, the tail
+        zero) so a reduce-scatter over equal rank blocks needs no copy."""
         cols = self._columns(pid, pk, value, num_privacy_ids, num_partitions)
         bp = self._bound_params(cfg, 0 if sync else native.BOUND_ASYNC)
         fields = Partials.fields_for(cfg.metrics_mask)
         P = max(int(num_partitions), 1)
-        parts = Partials(self.torch.empty((len(fields), P), dtype=self.torch.int64, device=self.device), fields,
-                         num_partitions)
+        W = max(P, int(padded or 0))
+        data = self.torch.empty((len(fields), W), dtype=self.torch.int64, device=self.device)
+        if W > P:
+            data[:, P:].zero_()
+        parts = Partials(data, fields, num_partitions)
         nbytes = ctypes.c_size_t(0)
         native.check(self.lib.pdp_workspace_size(ctypes.byref(cols), ctypes.byref(bp), ctypes.byref(nbytes)),
                      "pdp_workspace_size")

@@ -33,6 +33,8 @@ DEBUG_ANA_PACK = 64
 DEBUG_ANA_FLAGS = 128
 DEBUG_ANA_SEL_LDS = 256
 DEBUG_DEV_OCC3 = 512
+DEBUG_K4_COMPACT = 1024  # K2 claims compacted K4 pair slots (one atomic counter; measured slower)
+DEBUG_THIN2 = 67108864  # K4 on: the LDS-staged k_thin2 instead of k_thin (measured slower)
 
 c_i32, c_i64, c_u64, c_f64 = ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64, ctypes.c_double
 c_vp = ctypes.c_void_p

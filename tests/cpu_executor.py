@@ -63,7 +63,7 @@ class CpuExecutor:
             acc.nsumsq = y
         return _Acc(self.torch, acc, cfg.metrics_mask, num_partitions)
 
-    def accumulate_partials(self, pid, pk, value, num_privacy_ids, num_partitions, cfg, sync=True):
+    def accumulate_partials(self, pid, pk, value, num_privacy_ids, num_partitions, cfg, sync=True, padded=None):
         """pdp_bound_accumulate_partials restated: the oracle's kept pairs in
         K4's exported fixed point (pdp_oracle.k4_partials)."""
         from pipelinedp_amd.executor import Partials

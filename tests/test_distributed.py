@@ -48,14 +48,17 @@ class OracleExecutor:
     signatures, computed by the CPU oracle on torch CPU tensors (test
     infrastructure only)."""
 
-    def accumulate_partials(self, pid, pk, value, num_privacy_ids, num_partitions, bounds, sync=True):
+    def accumulate_partials(self, pid, pk, value, num_privacy_ids, num_partitions, bounds, sync=True, padded=None):
         import torch
 
         from pipelinedp_amd.executor import Partials
         acc = o.bound_and_accumulate(pid.numpy(), pk.numpy(), value.numpy(), num_partitions, BP, "hash", seed=5)
         parts = o.k4_partials(acc, num_partitions, BP, MASK)
         fields = Partials.fields_for(MASK)
-        return Partials(torch.from_numpy(np.stack([parts[f] for f in fields])), fields, num_partitions)
+        data = np.stack([parts[f] for f in fields])
+        if padded and padded > num_partitions:  # HipExecutor's padded columns (reduce-scatter without a copy)
+            data = np.concatenate([data, np.full((len(fields), padded - num_partitions), -1, np.int64)], axis=1)
+        return Partials(torch.from_numpy(data), fields, num_partitions)
 
     def finalize_partials(self, parts, bounds):
         import torch

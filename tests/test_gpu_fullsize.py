@@ -364,3 +364,52 @@ def test_c2_public_partitions_full_size(ex):
     assert torch.equal(acc2.row_count, rc)
     assert torch.equal(acc2.count, cnt)
     assert bool(((acc2.x - sm).abs() <= 1e-9 * (b * cnt.to(torch.float64) + 1.0)).all())
+
+
+def test_more_than_2_32_rows_k4_equals_two_halves(ex):
+    """4.4e9 rows (> 2^32) in ONE call keep K4's fixed-point reduction (round
+    4 fell back to fp64 atomics at >= 2^32 rows): privacy id = row // 16, each
+    privacy id's 16 rows in 16 distinct partitions (pk = 7919 row mod P), so
+    with L0 = 4 every privacy id keeps exactly 4 single-row pairs:
+    sum(row_count) == sum(count) == 4 U.  Two privacy-id-disjoint halves
+    (< 2^32 rows each) through pdp_bound_accumulate_partials, summed, give
+    the same accumulators bit for bit -- the merge of pipeline_backend.py:528-538
+    whatever the split.  COUNT + PRIVACY_ID_COUNT (no value column: 16 B/row,
+    70 GB of input + ~160 GB of workspace)."""
+    import torch
+    from pipelinedp_amd.executor import BoundConfig
+    n, P, L0, Linf = 4_400_000_000, 1_000_000, 4, 1
+    U = n // 16
+    assert n > (1 << 32) and (n // 2) < (1 << 32)
+    dev = torch.device("cuda", 0)
+    # built in slices: this torch build's elementwise kernels (arange, ...) fill only numel mod 2^32
+    # elements of a tensor with more than 2^32 (round 5, tools/diag_big3.py)
+    C = 1 << 30
+    pid = torch.empty(n, dtype=torch.int64, device=dev)
+    pk = torch.empty(n, dtype=torch.int64, device=dev)
+    per_pk = torch.zeros(P, dtype=torch.int64, device=dev)
+    for c0 in range(0, n, C):
+        r = torch.arange(c0, min(n, c0 + C), dtype=torch.int64, device=dev)
+        pid[c0:c0 + r.numel()] = r // 16
+        pk[c0:c0 + r.numel()] = r.mul_(7919).remainder_(P)
+        per_pk += torch.bincount(pk[c0:c0 + r.numel()], minlength=P)
+        del r
+    assert int(pid[-1]) == (n - 1) // 16 and int(pk[-1]) == (n - 1) * 7919 % P
+    cfg = BoundConfig(MASK_COUNT | MASK_PID, L0, Linf, sampling_seed=5)
+    acc = ex.accumulate(pid, pk, None, U, P, cfg)
+    torch.cuda.synchronize()
+    st = ex.stats()
+    assert st.k4_pairs == 4 * U and st.fallback_rows == 0
+    rc, cnt = acc.row_count.clone(), acc.count.clone()
+    del acc
+    assert int(rc.sum()) == 4 * U and int(cnt.sum()) == 4 * U
+    assert torch.equal(rc, cnt)  # every kept pair is one row
+    assert bool((rc <= per_pk).all())
+    h = n // 2  # a multiple of 16: the halves share no privacy id
+    total = None
+    for lo in (0, h):
+        parts = ex.accumulate_partials(pid[lo:lo + h], pk[lo:lo + h], None, U, P, cfg)
+        total = parts.data.clone() if total is None else total + parts.data
+        del parts
+    torch.cuda.synchronize()
+    assert torch.equal(total[0], rc) and torch.equal(total[1], cnt)

@@ -622,13 +622,17 @@ def test_k4_pair_record_forms_bitwise_equal(ex, cfgi):
     (debug flag K4_P16 forces them); K2 can write the 12-byte form as split slots
     (keys, then values: the first pass reads 4 bytes of an empty slot; flag
     K4_SOA): the fixed-point sums are integers, so all three forms give
-    identical accumulators, sums included."""
+    identical accumulators, sums included.  So do the K2 forms under the L0
+    pre-filter (forced on at these sizes): k_thin (default) and the LDS-staged
+    k_thin2 (THIN2), each writing a slot per row (default) or compacted pair
+    records (K4_COMPACT)."""
     n, U, P, z, L0, Linf, vb, pb, mask = CONFIGS[cfgi]
     pid, pk, val = o.synth_rows(n, U, P, seed=700 + cfgi, zipf_s=z, value_lo=-5, value_hi=15)
     bp = o.BoundParams(L0, Linf, *(vb or (None, None)), *(pb or (None, None)))
     need_val = bool(mask & (2 | 4 | 8))
     runs = []
-    for form in (K4_SOA, 0, K4_P16 | K4_SOA):
+    ff, compact, thin2 = 268435456, 1024, 67108864  # FORCE_FILTER, K4_COMPACT, THIN2
+    for form in (K4_SOA, 0, K4_P16 | K4_SOA, compact, ff, ff | compact, ff | thin2, ff | thin2 | compact):
         _, _, rc, cnt, x, y = run_gpu(ex, pid, pk, val if need_val else None, U, P, bp, mask, seed=5 + cfgi,
                                       debug_flags=form)
         runs.append((rc, cnt, x, y))

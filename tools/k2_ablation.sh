@@ -1,7 +1,7 @@
 #!/bin/bash
 # K2 ablations on the GPU box: per-stage times of bench.py under debug flags
 # (262144 no accumulator atomics, 1048576 L0 by minimum searches, 8388608 no L_inf
-# ranking, 16777216 no kept-row sums, 33554432 LDS cache forced on, 67108864 4096-block grid,
+# ranking, 16777216 no kept-row sums, 33554432 LDS cache forced on, 67108864 k_thin v1 (was: 4096-block grid),
 # 2097152 segment walk only).  Output: gpurun_out/k2abl/<workload>_<flags>.json
 set -e
 export TMPDIR=/tmp
