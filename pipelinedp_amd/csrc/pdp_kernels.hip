@@ -217,6 +217,14 @@ struct SegParams {
   int k4passes;
   int k4shift[3];
   int k4bits[3];
+  // K4 hot-partition table (pdp_reduce.inc, K4Hot): k4hot != 0 -- the K2 kernel holds a per-block LDS
+  // table whose pairs are added in fixed point (q = rint(x * k4q)) and flushed with integer atomics
+  // into the accumulators' counts and K4's fixed-point scratch k4glo / k4ghi / k4gfl.
+  int k4hot;
+  double k4q;
+  unsigned long long* k4glo;
+  unsigned long long* k4ghi;
+  unsigned int* k4gfl;
 };
 
 constexpr int kDebugBatchKernel = 4096;  // use k_segments even when k_lean applies
@@ -230,7 +238,7 @@ constexpr int kDebugLinearWrite = 65536;
 constexpr int kDebugNoScatter = 2048;  // with kDebugSortOnly: the radix passes stage in LDS but store nothing
 constexpr int kDebugLookback = 131072;  // radix passes by decoupled look-back instead of reduce-then-scan
 constexpr int kDebugNoAtomics = 262144;  // K2 skips its accumulator atomics (timing ablation)
-constexpr int kDebugNoHotCache = 524288;  // k_lean emits straight to HBM (no LDS partition cache)
+constexpr int kDebugNoHotCache = 524288;  // K2 without its LDS hot-partition table (K4 off: HotCache; on: K4Hot)
 constexpr int kDebugLeanMinSearch = 1048576;  // k_lean ranks L0 by minimum searches even when L0 >= kSortMinL0
 constexpr int kDebugWalkOnly = 2097152;  // k_lean loads rows and finds segments only (timing floor, results invalid)
 constexpr int kDebugNoLinf = 8388608;     // k_lean skips the L_inf ranking (timing ablation, results invalid)
@@ -254,7 +262,7 @@ constexpr int kDebugAnaNpartAtomics = 32;   // utility analysis: n_partitions by
 constexpr int kDebugAnaPack = 64;           // utility analysis: separate pack kernel before the sort
 constexpr int kDebugAnaFlags = 128;         // utility analysis: round-3 per-row flags + scan pair extraction
 constexpr int kDebugAnaSelLds = 256;        // utility analysis: round-3 per-regime selection kernels
-constexpr int kDebugDevOcc3 = 512;          // device-sized look-back passes at 3 blocks per CU (spills)
+constexpr int kDebugDevOcc2 = 512;          // device-sized look-back passes at 2 blocks per CU (no spills, slower)
 constexpr int kDebugK4Compact = 1024;       // K2 writes compacted K4 pair records (k4_claim) instead of a slot per row
 // Timing ablations whose results are invalid: accepted only by a -DPDP_DEBUG_BUILD library.
 constexpr int kAblationFlags = kDebugSortOnly | kDebugNoLookback | kDebugLinearWrite | kDebugNoScatter |
@@ -1130,10 +1138,11 @@ __device__ __forceinline__ bool onesweep_body(
 // Launches whose tile count the host knows run one tile per block.  The passes over a row count that
 // lives in device memory (the survivor sort, K4's pair passes) loop over tiles claimed in order, so a
 // grid sized from a host bound covers every tile.  The loop costs registers (round 5: 80-108 B of
-// scratch at 3 blocks per CU; none at 2), so only those kernels have it, at 2 blocks per CU (debug flag
-// DEV_OCC3: 3).
-#define PDP_ONESWEEP_LOOP(...)                         \
-  while (__VA_ARGS__(PDP_ONESWEEP_PASS) && !tile_base) \
+// scratch at 3 blocks per CU; none at 2), so only those kernels have it.  3 blocks per CU nevertheless
+// (r05f: c4 pair passes 9.25 -> 7.62 ms, c3 survivor sort 1.94 -> 1.81 ms against 2; debug flag
+// DEV_OCC2: 2, debug library PDP_DEV_OCC=2|3|4).
+#define PDP_ONESWEEP_LOOP(B, ...)                        \
+  while (B<__VA_ARGS__>(PDP_ONESWEEP_PASS) && !tile_base) \
     __syncthreads();
 // records -> records (passes >= 1 of the pid sort, generic path, utility analysis)
 __global__ __launch_bounds__(kThreads, PDP_OS_OCC) void k_onesweep(PDP_ONESWEEP_ARGS) {
@@ -1142,7 +1151,7 @@ __global__ __launch_bounds__(kThreads, PDP_OS_OCC) void k_onesweep(PDP_ONESWEEP_
 // ... over a device-side record count (the L0 pre-filter's survivors)
 template <int OCC>
 __global__ __launch_bounds__(kThreads, OCC) void k_onesweep_dev(PDP_ONESWEEP_ARGS) {
-  PDP_ONESWEEP_LOOP(onesweep_body<false, false>)
+  PDP_ONESWEEP_LOOP(onesweep_body, false, false, 0, false)
 }
 // SoA columns -> records (first pass of the pid sort, non-public rows dropped)
 __global__ __launch_bounds__(kThreads, PDP_OS_OCC) void k_sort_first(PDP_ONESWEEP_ARGS) {
@@ -1159,17 +1168,17 @@ __global__ __launch_bounds__(kThreads, PDP_OS_OCC) void k_bucket_pass(PDP_ONESWE
 // K4 pair records by partition block (pdp_reduce.inc); device-side record counts
 template <int OCC>
 __global__ __launch_bounds__(kThreads, OCC) void k_pair_pass(PDP_ONESWEEP_ARGS) {
-  PDP_ONESWEEP_LOOP(onesweep_body<false, false>)
+  PDP_ONESWEEP_LOOP(onesweep_body, false, false, 0, false)
 }
 // ... with 12-byte pair records (K2 writes its slots in that form)
 template <int OCC>
 __global__ __launch_bounds__(kThreads, OCC) void k_pair_pass12(PDP_ONESWEEP_ARGS) {
-  PDP_ONESWEEP_LOOP(onesweep_body<false, false, 2>)
+  PDP_ONESWEEP_LOOP(onesweep_body, false, false, 2, false)
 }
 // ... whose first pass reads K2's split slots (keys, then the values of the non-empty ones)
 template <int OCC>
 __global__ __launch_bounds__(kThreads, OCC) void k_pair_pass12s(PDP_ONESWEEP_ARGS) {
-  PDP_ONESWEEP_LOOP(onesweep_body<false, false, 3>)
+  PDP_ONESWEEP_LOOP(onesweep_body, false, false, 3, false)
 }
 
 // Clears the look-back status words of the tiles of *rows_dev + add rows (a row count that lives in
@@ -2037,6 +2046,7 @@ struct ProfScope {
 };
 
 int env_int(const char* name, int def);
+int dev_occ(int debug);
 
 // Look-back status words carry the epoch of their pass, so a region cleared
 // once serves 0xFFFE passes.  The region is cleared again when a pass needs
@@ -2172,7 +2182,8 @@ int sort_recs(pdp_ctx* ctx, Rec* a, Rec* b, int64_t m, const KeySpec& ks, unsign
       if (rc) return rc;
     }
     const bool soa = soa_pk && p == 0;
-    auto dev_kern = (ctx->cur_debug & kDebugDevOcc3) ? k_onesweep_dev<3> : k_onesweep_dev<2>;
+    const int occ = dev_occ(ctx->cur_debug);
+    auto dev_kern = occ == 2 ? k_onesweep_dev<2> : occ == 4 ? k_onesweep_dev<4> : k_onesweep_dev<3>;
     hipLaunchKernelGGL(soa ? k_ana_sort_first : m_dev ? dev_kern : k_onesweep, dim3(grid), dim3(kThreads), 0, stream,
                        soa ? soa_pid : (const int64_t*)nullptr, soa ? soa_pk : (const int64_t*)nullptr,
                        soa ? soa_val : (const double*)nullptr, soa ? (const Rec*)nullptr : src, dst, m,
@@ -2569,6 +2580,12 @@ int env_int(const char* name, int def) {
   return v && *v ? std::atoi(v) : def;
 }
 
+// Blocks per CU of the device-sized look-back passes (PDP_ONESWEEP_LOOP kernels).
+int dev_occ(int debug) {
+  if (debug & kDebugDevOcc2) return 2;
+  return env_int("PDP_DEV_OCC", 3);
+}
+
 FilterPlan filter_plan(int64_t n, int64_t U, const pdp_bound_params* bp, int debug, bool sweep, bool rts) {
   FilterPlan f{};
   if (sweep || !rts || bp->bounds_already_enforced || (debug & kDebugNoFilter)) return f;
@@ -2691,6 +2708,11 @@ int k4_run(pdp_ctx* ctx, hipStream_t stream, const K4Plan& k, const K4Red& kr, b
            unsigned long long* s_lo, unsigned long long* s_hi, unsigned int* s_fl, int64_t buf_cap,
            int64_t soa_a = 0, int64_t soa_b = 0) {
   const int64_t upper = upper_a + len_b;
+  // K2's hot-partition tables: every partition's sum from their scratch first (k4_reduce rewrites the
+  // partitions it sees with the complete sums)
+  if (kr.addg && kr.want_x && !y)
+    hipLaunchKernelGGL(k4_convert_all, dim3(grid_for(kr.P, kThreads, 4096)), dim3(kThreads), 0, stream, kr, acc,
+                       s_lo, s_hi, s_fl);
   if (upper == 0) return 0;
   // in_a's count: counters[a_slot], or exactly upper_a (a host count) when a_slot < 0
   hipLaunchKernelGGL(k4_total, dim3(1), dim3(64), 0, stream, counters, a_slot,
@@ -2724,10 +2746,10 @@ int k4_run(pdp_ctx* ctx, hipStream_t stream, const K4Plan& k, const K4Red& kr, b
       // n_eff - len_b (onesweep_body); without in_b nothing is read from rin2
       const int64_t split = p == 0 && in_b ? -len_b - 1 : (int64_t)INT64_MAX;
       next_epoch_dev(ctx, stream, status, counters + kCtrK4In, 0, p == 0);
-      const bool o3 = (ctx->cur_debug & kDebugDevOcc3) != 0;
-      auto pass_kern = k.p12 ? (p == 0 && k.soa ? (o3 ? k_pair_pass12s<3> : k_pair_pass12s<2>)
-                                                : (o3 ? k_pair_pass12<3> : k_pair_pass12<2>))
-                             : (o3 ? k_pair_pass<3> : k_pair_pass<2>);
+      const int occ = dev_occ(ctx->cur_debug);
+      auto pass_kern = k.p12 ? (p == 0 && k.soa ? (occ == 2 ? k_pair_pass12s<2> : occ == 4 ? k_pair_pass12s<4> : k_pair_pass12s<3>)
+                                                : (occ == 2 ? k_pair_pass12<2> : occ == 4 ? k_pair_pass12<4> : k_pair_pass12<3>))
+                             : (occ == 2 ? k_pair_pass<2> : occ == 4 ? k_pair_pass<4> : k_pair_pass<3>);
       hipLaunchKernelGGL(pass_kern, dim3(grid), dim3(kThreads), 0, stream, (const int64_t*)nullptr,
                          (const int64_t*)nullptr, (const double*)nullptr, src, dst, (int64_t)0, counters, n_slot,
                          ks, p, off + p * kHist, status, ctx->epoch, counters, (int)ctx->tile_slot++,
@@ -2742,7 +2764,7 @@ int k4_run(pdp_ctx* ctx, hipStream_t stream, const K4Plan& k, const K4Red& kr, b
   kd.chunk = 0;  // counters[kCtrK4Chunk] (k4_total)
   const unsigned cgrid = (unsigned)std::min<int64_t>((upper + 4095) / 4096, 1024);
   const bool scratch = y || kr.want_x;
-  if (scratch)
+  if (scratch && !kr.addg)  // (with the hot tables the scratch was zeroed for the whole call)
     hipLaunchKernelGGL(k.p12 ? k4_zero_shared<1> : k4_zero_shared<0>, dim3(cgrid), dim3(kThreads), 0, stream, src,
                        counters, kr.sh, kr.P, (int64_t)0, s_lo, s_hi, s_fl, kr.cb);
   auto pick = [&](auto k12, auto k11) { return kr.sh == kK4ShMax ? k12 : k11; };
@@ -2943,6 +2965,7 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
     ctx->stats.k4_passes = k4.passes;
     // records per reduce chunk: counters[kCtrK4Chunk] (k4_total: ~1024 chunks, 4096 .. 32768)
     K4Red krx = k4_red(k4, q, P, false), kry = k4_red(k4, q, P, true);
+    krx.addg = q.k4hot;  // the hot tables' fixed-point scratch (x run; not with VARIANCE)
     if (parts) {  // fixed-point export (multi-GPU partials)
       krx.fxh = (long long*)parts->x_hi;
       krx.fxl = (long long*)parts->x_lo;
@@ -3138,6 +3161,20 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
   // k_thin2 +1.3 ms for a 0.26 ms shorter first pair pass; c4 k_lean 8.56 -> 150 ms).
   k4_compact = k4.on && (sp.debug & kDebugK4Compact);
   k4_attach(sp, spare, k4_compact);
+  const bool lean = !thin && bp->max_partitions_contributed <= kLeanMaxL0 && !(sp.debug & kDebugBatchKernel);
+  // K4 hot-partition tables (pdp_reduce.inc, K4Hot) in k_thin / k_lean: not with VARIANCE (one
+  // fixed-point scratch), the sweep or the debug forms; debug flag NO_HOT_CACHE turns them off
+  const bool k4hot = k4.on && !sweep && !k4_compact && !thin2 && !sp.want_y && (thin || lean) &&
+                     !(sp.debug & kDebugNoHotCache);
+  sp.k4hot = k4hot ? 1 : 0;
+  if (k4hot) {
+    sp.k4q = std::ldexp(1.0, k4.fx);
+    sp.k4glo = k4lo;
+    sp.k4ghi = k4hi;
+    sp.k4gfl = k4fl;
+    HIP_TRY(zero_async(k4lo, (size_t)P * 16, stream));  // lo, hi
+    HIP_TRY(zero_async(k4fl, ((size_t)P * 4 + 7) / 8 * 8, stream));
+  }
   if (c > 0) {
     // fresh K2/KF counters; the kept-row count of the shared sort stays
     unsigned long long reset[kCtrSweepCycles] = {};
@@ -3158,6 +3195,8 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
           std::max<int64_t>(1, std::min<int64_t>((waves + 3) / 4, (sp.debug & kDebugOddGrid) ? 7 : 8192));
       const int64_t l0 = bp->max_partitions_contributed;
       auto kern = v2 ? (l0 <= 1 ? k_thin2<1> : l0 <= 2 ? k_thin2<2> : l0 <= 4 ? k_thin2<4> : k_thin2<8>)
+                : k4hot ? (l0 <= 1 ? k_thin<false, 1, false, true> : l0 <= 2 ? k_thin<false, 2, false, true>
+                           : l0 <= 4 ? k_thin<false, 4, false, true> : k_thin<false, 8, false, true>)
                 : k4_compact ? (l0 <= 1 ? k_thin<false, 1, true> : l0 <= 2 ? k_thin<false, 2, true>
                                 : l0 <= 4 ? k_thin<false, 4, true> : k_thin<false, 8, true>)
                 : l0 <= 1 ? (tcache ? k_thin<true, 1> : k_thin<false, 1>)
@@ -3166,7 +3205,7 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
                           : (tcache ? k_thin<true, 8> : k_thin<false, 8>);
       hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), 0, stream, sorted, counters, n_slot, sp, acc, ov, big,
                          (int)bp->debug_force_fallback);
-    } else if (bp->max_partitions_contributed <= kLeanMaxL0 && !(sp.debug & kDebugBatchKernel)) {
+    } else if (lean) {
       const int64_t waves = ((int64_t)n_sorted + kLeanChunk - 1) / kLeanChunk;
       int64_t max_blocks = kLeanMaxBlocks;
       if (sp.debug & kDebugOddGrid) max_blocks = 5;
@@ -3179,7 +3218,9 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
                           false) &&
                          !(sp.debug & kDebugNoHotCache);
       const bool two = bp->max_partitions_contributed > 64;
-      auto kern = sorted_l0 ? (two ? (cache ? k_lean<2, true, true> : k_lean<2, true, false>)
+      auto kern = k4hot ? (sorted_l0 ? (two ? k_lean<2, true, false, true> : k_lean<1, true, false, true>)
+                                     : (two ? k_lean<2, false, false, true> : k_lean<1, false, false, true>))
+                : sorted_l0 ? (two ? (cache ? k_lean<2, true, true> : k_lean<2, true, false>)
                                    : (cache ? k_lean<1, true, true> : k_lean<1, true, false>))
                             : (two ? (cache ? k_lean<2, false, true> : k_lean<2, false, false>)
                                    : (cache ? k_lean<1, false, true> : k_lean<1, false, false>));

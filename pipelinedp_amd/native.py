@@ -32,9 +32,10 @@ DEBUG_ANA_NPART_ATOMICS = 32
 DEBUG_ANA_PACK = 64
 DEBUG_ANA_FLAGS = 128
 DEBUG_ANA_SEL_LDS = 256
-DEBUG_DEV_OCC3 = 512
+DEBUG_DEV_OCC2 = 512  # device-sized look-back passes at 2 blocks per CU
 DEBUG_K4_COMPACT = 1024  # K2 claims compacted K4 pair slots (one atomic counter; measured slower)
 DEBUG_THIN2 = 67108864  # K4 on: the LDS-staged k_thin2 instead of k_thin (measured slower)
+DEBUG_NO_HOT_CACHE = 524288  # K2 without its hot-partition table (K4 off: LDS atomics cache; K4 on: K4Hot)
 
 c_i32, c_i64, c_u64, c_f64 = ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64, ctypes.c_double
 c_vp = ctypes.c_void_p

@@ -625,14 +625,16 @@ def test_k4_pair_record_forms_bitwise_equal(ex, cfgi):
     identical accumulators, sums included.  So do the K2 forms under the L0
     pre-filter (forced on at these sizes): k_thin (default) and the LDS-staged
     k_thin2 (THIN2), each writing a slot per row (default) or compacted pair
-    records (K4_COMPACT)."""
+    records (K4_COMPACT); and with or without K2's hot-partition tables
+    (NO_HOT_CACHE: every kept pair a record)."""
     n, U, P, z, L0, Linf, vb, pb, mask = CONFIGS[cfgi]
     pid, pk, val = o.synth_rows(n, U, P, seed=700 + cfgi, zipf_s=z, value_lo=-5, value_hi=15)
     bp = o.BoundParams(L0, Linf, *(vb or (None, None)), *(pb or (None, None)))
     need_val = bool(mask & (2 | 4 | 8))
     runs = []
-    ff, compact, thin2 = 268435456, 1024, 67108864  # FORCE_FILTER, K4_COMPACT, THIN2
-    for form in (K4_SOA, 0, K4_P16 | K4_SOA, compact, ff, ff | compact, ff | thin2, ff | thin2 | compact):
+    ff, compact, thin2, nohot = 268435456, 1024, 67108864, 524288  # FORCE_FILTER, K4_COMPACT, THIN2, NO_HOT_CACHE
+    for form in (K4_SOA, 0, K4_P16 | K4_SOA, compact, nohot, ff, ff | compact, ff | thin2, ff | thin2 | compact,
+                 ff | nohot):
         _, _, rc, cnt, x, y = run_gpu(ex, pid, pk, val if need_val else None, U, P, bp, mask, seed=5 + cfgi,
                                       debug_flags=form)
         runs.append((rc, cnt, x, y))
