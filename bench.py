@@ -27,6 +27,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+GUIDE_COPY_GBS = 6290.0  # MI355X_MICROARCH.md:36, measured device copy
 
 # Per-GPU shapes of BASELINE.json configs (SURVEY.md 8(d) "Synthetic inputs").
 # c3 is the headline: COUNT+SUM+MEAN, private selection, 1e9 rows / 1e6 Zipf partitions.
@@ -513,6 +514,12 @@ def main():
                                       "next to the 8 TB/s spec peak")
         if copy_gbs and roofline.get("unit") == "GB/s":
             roofline["frac_of_copy"] = round(roofline["achieved"] / copy_gbs, 4)
+        if roofline.get("unit") == "GB/s":
+            # the guide's measured device copy (the stricter ceiling than this build's own probe)
+            roofline["guide_copy"] = GUIDE_COPY_GBS
+            roofline["frac_of_guide_copy"] = round(roofline["achieved"] / GUIDE_COPY_GBS, 4)
+            roofline["guide_copy_note"] = "device-to-device copy measured by /opt/skills/guides/MI355X_MICROARCH.md:36"
+
     if rank == 0:
         e2e = rows_per_s * 24 / 1e9
         line = {

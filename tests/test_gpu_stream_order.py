@@ -61,7 +61,9 @@ def test_one_host_wait_per_call_and_none_async(ex):
     assert ex.status() == 0
     st2 = ex.stats()
     assert st2.host_waits == 0
-    assert st2.filter_rows == st.filter_rows and st2.k4_pairs == st.k4_pairs
+    # (k4_pairs, the records that reach K4's pair passes, depends on which partitions claimed K2's
+    # hot-partition slots first; the accumulators do not)
+    assert st2.filter_rows == st.filter_rows
     for name in ("row_count", "count", "x"):
         assert torch.equal(getattr(a1, name), getattr(a2, name)), name
     ref = o.bound_and_accumulate(pid, pk, val, P, o.BoundParams(4, 2, 0.0, 10.0), "hash", seed=7)
