@@ -3164,7 +3164,9 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
   const bool lean = !thin && bp->max_partitions_contributed <= kLeanMaxL0 && !(sp.debug & kDebugBatchKernel);
   // K4 hot-partition tables (pdp_reduce.inc, K4Hot) in k_thin / k_lean: not with VARIANCE (one
   // fixed-point scratch), the sweep or the debug forms; debug flag NO_HOT_CACHE turns them off
-  const bool k4hot = k4.on && !sweep && !k4_compact && !thin2 && !sp.want_y && (thin || lean) &&
+  // k_lean only: in k_thin (L0 <= 8: few pairs per privacy id) the tables cost the kernel about what they
+  // save K4 (r05j c3: K2 +0.20 ms, K4 -0.15 ms); at c4 (L0 = 32) they pay (K2 +1.1, K4 -2.2 ms)
+  const bool k4hot = k4.on && !sweep && !k4_compact && !thin2 && !sp.want_y && lean &&
                      !(sp.debug & kDebugNoHotCache);
   sp.k4hot = k4hot ? 1 : 0;
   if (k4hot) {
@@ -3191,8 +3193,11 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
       // LDS partition cache on: the Zipf-head pairs' HBM atomics otherwise dominate (c3: K2 8.1 -> 3.4 ms);
       // K4 writes pair records instead of atomics, no cache
       const bool tcache = !k4.on;
+      // the grid is sized from the row count, an upper bound of the survivors: capped at 2048 blocks
+      // (8 per CU), so a small share (one rank's part of a multi-GPU step) does not pay 8192 blocks'
+      // K4 histogram flushes
       const int64_t blocks =
-          std::max<int64_t>(1, std::min<int64_t>((waves + 3) / 4, (sp.debug & kDebugOddGrid) ? 7 : 8192));
+          std::max<int64_t>(1, std::min<int64_t>((waves + 3) / 4, (sp.debug & kDebugOddGrid) ? 7 : kThinMaxBlocks));
       const int64_t l0 = bp->max_partitions_contributed;
       auto kern = v2 ? (l0 <= 1 ? k_thin2<1> : l0 <= 2 ? k_thin2<2> : l0 <= 4 ? k_thin2<4> : k_thin2<8>)
                 : k4hot ? (l0 <= 1 ? k_thin<false, 1, false, true> : l0 <= 2 ? k_thin<false, 2, false, true>
