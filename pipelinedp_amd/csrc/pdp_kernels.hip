@@ -3193,9 +3193,6 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
       // LDS partition cache on: the Zipf-head pairs' HBM atomics otherwise dominate (c3: K2 8.1 -> 3.4 ms);
       // K4 writes pair records instead of atomics, no cache
       const bool tcache = !k4.on;
-      // the grid is sized from the row count, an upper bound of the survivors: capped at 2048 blocks
-      // (8 per CU), so a small share (one rank's part of a multi-GPU step) does not pay 8192 blocks'
-      // K4 histogram flushes
       const int64_t blocks =
           std::max<int64_t>(1, std::min<int64_t>((waves + 3) / 4, (sp.debug & kDebugOddGrid) ? 7 : kThinMaxBlocks));
       const int64_t l0 = bp->max_partitions_contributed;

@@ -16,11 +16,19 @@ depend on the rank count either.
 
 The collective backend is whatever ``torch.distributed`` was initialised
 with: ``nccl`` (= RCCL over xGMI on MI355X) for GPUs, ``gloo`` in CPU tests.
+
+Restriction: the exported partials need K4's fixed point, which runs for
+every input except a rank-local share of >= 2^32 rows with L_inf >= 131072
+(and the testing-only debug flag NO_K4).  World.aggregate checks this before
+any collective and raises ValueError, on every rank alike (the condition
+depends only on the bounds and the agreed row counts); there is no fp64
+fallback, whose sums would depend on the reduction order.
 """
 import dataclasses
 from typing import Optional
 
 PID_SHARD_SALT = 0x9E3779B97F4A7C15
+K4_MAX_LINF_BEYOND_2_32 = 131072  # pdp_kernels.hip k4_enabled: (2^32) / kK4Chunk
 
 
 def shard_of(pid, world_size: int):
@@ -171,9 +179,19 @@ class World:
         not wait for the stream (check ``ex.status()`` after it drained).  Returns (keep [P], metrics [F, P], fields) of
         ALL partitions on every rank when ``gather`` (all-gather of the owned
         blocks), else of the owned block only."""
+        import torch
         import torch.distributed as dist
         if shuffle and pid is not None:
             pid, pk, value = self.shuffle_by_privacy_id(ex, pid, pk, value)
+        linf = int(getattr(bounds, "max_contributions_per_partition", 1) or 1)
+        if linf >= K4_MAX_LINF_BEYOND_2_32:
+            n_local = torch.tensor([int(pk.numel()) if pk is not None else 0], dtype=torch.int64)
+            if dist.get_backend(self.group) == "nccl":
+                n_local = n_local.cuda()
+            dist.all_reduce(n_local, op=dist.ReduceOp.MAX, group=self.group)
+            if int(n_local.item()) >= 1 << 32:
+                raise ValueError(f"multi-GPU partials need K4's fixed point: a rank-local share of >= 2^32 rows "
+                                 f"needs max_contributions_per_partition < {K4_MAX_LINF_BEYOND_2_32} (got {linf})")
         off, length, padded = self.block(num_partitions)
         parts = ex.accumulate_partials(pid, pk, value, num_privacy_ids, num_partitions, bounds, sync=sync,
                                        padded=padded)

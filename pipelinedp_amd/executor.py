@@ -51,15 +51,20 @@ def _ptr(t):
 class Accumulators:
     """Dense per-partition accumulators on the device."""
 
-    def __init__(self, torch, num_partitions: int, device, metrics_mask: int):
+    def __init__(self, torch, num_partitions: int, device, metrics_mask: int, counts=None):
+        """counts: (row_count, count) tensors to use instead of allocating them (finalize_partials
+        reuses the summed partials' rows)."""
         m = metrics_mask
         i64, f64 = torch.int64, torch.float64
         P = max(int(num_partitions), 1)
         self.num_partitions = int(num_partitions)
-        self.row_count = torch.empty(P, dtype=i64, device=device)
         need_count = bool(m & (native.METRIC_COUNT | native.METRIC_MEAN | native.METRIC_VARIANCE))
         need_x = bool(m & (native.METRIC_SUM | native.METRIC_MEAN | native.METRIC_VARIANCE))
-        self.count = torch.empty(P, dtype=i64, device=device) if need_count else None
+        if counts is not None:
+            self.row_count, self.count = counts[0], counts[1] if need_count else None
+        else:
+            self.row_count = torch.empty(P, dtype=i64, device=device)
+            self.count = torch.empty(P, dtype=i64, device=device) if need_count else None
         self.x = torch.empty(P, dtype=f64, device=device) if need_x else None
         self.y = torch.empty(P, dtype=f64, device=device) if m & native.METRIC_VARIANCE else None
 
@@ -209,10 +214,8 @@ class HipExecutor:
     def finalize_partials(self, parts: Partials, cfg: BoundConfig) -> Accumulators:
         """pdp_finalize_partials: (summed) partials -> Accumulators for release."""
         P = parts.num_partitions
-        acc = Accumulators(self.torch, P, self.device, cfg.metrics_mask)
-        acc.row_count = parts.row("row_count")
-        if acc.count is not None:
-            acc.count = parts.row("count")
+        acc = Accumulators(self.torch, P, self.device, cfg.metrics_mask,
+                           counts=(parts.row("row_count"), parts.row("count")))
         bp = self._bound_params(cfg)
         ps, accs = parts.as_struct(), acc.as_struct()
         native.check(self.lib.pdp_finalize_partials(self.ctx, ctypes.byref(ps), P, ctypes.byref(bp),

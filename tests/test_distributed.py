@@ -320,3 +320,30 @@ def test_many_privacy_ids_two_ranks_no_key_exchange_bitwise(tmp_path):
             np.testing.assert_array_equal(g, w)
     acc_rows = [c[1] for r in runs for c in r["calls"] if c[0] == "accumulate"]
     assert sum(acc_rows) == len(rows)
+
+
+def test_aggregate_refuses_partials_k4_cannot_make(tmp_path):
+    """A rank-local share of >= 2^32 rows with L_inf >= 131072 has no fixed-point
+    partials (pdp_kernels.hip k4_enabled): World.aggregate raises before any
+    accumulate or data collective (world size 1, gloo; the row count is a stub)."""
+    import torch
+    import torch.distributed as dist
+
+    from pipelinedp_amd.distributed import World
+    from pipelinedp_amd.executor import BoundConfig
+
+    class Huge:  # numel() only: the check must not touch the rows
+        def numel(self):
+            return 1 << 32
+
+    class NoAccumulate:
+        def accumulate_partials(self, *a, **k):
+            raise AssertionError("must not accumulate")
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0, world_size=1)
+    try:
+        w = World(0, 1)
+        with pytest.raises(ValueError, match="2\\^32"):
+            w.aggregate(NoAccumulate(), None, Huge(), None, 10, 10, BoundConfig(1, 1, 131072), None)
+    finally:
+        dist.destroy_process_group()
