@@ -3166,8 +3166,8 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
   // fixed-point scratch), the sweep or the debug forms; debug flag NO_HOT_CACHE turns them off
   // k_lean only: in k_thin (L0 <= 8: few pairs per privacy id) the tables cost the kernel about what they
   // save K4 (r05j c3: K2 +0.20 ms, K4 -0.15 ms); at c4 (L0 = 32) they pay (K2 +1.1, K4 -2.2 ms)
-  const bool k4hot = k4.on && !sweep && !k4_compact && !thin2 && !sp.want_y && lean &&
-                     !(sp.debug & kDebugNoHotCache);
+  const bool k4hot = k4.on && !sweep && !k4_compact && !thin2 && !sp.want_y &&
+                     (lean || (thin && env_int("PDP_K4_HOT_THIN", 0))) && !(sp.debug & kDebugNoHotCache);
   sp.k4hot = k4hot ? 1 : 0;
   if (k4hot) {
     sp.k4q = std::ldexp(1.0, k4.fx);
