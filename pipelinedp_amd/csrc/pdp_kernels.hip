@@ -2070,7 +2070,10 @@ int next_epoch(pdp_ctx* ctx, hipStream_t stream, unsigned long long* status, siz
 // next_epoch for passes whose row count lives in device memory (*rows_dev + add): the clear is a
 // kernel sized by that count.  `fresh`: the first pass of a group (its tiles may exceed what earlier
 // passes of this call cleared).
-constexpr unsigned kPersistGrid = 2048;  // look-back launches over a device row count: blocks loop over tiles
+#ifndef PDP_PERSIST_GRID
+#define PDP_PERSIST_GRID 2048
+#endif
+constexpr unsigned kPersistGrid = PDP_PERSIST_GRID;  // look-back launches over a device row count: blocks loop over tiles
 void next_epoch_dev(pdp_ctx* ctx, hipStream_t stream, unsigned long long* status, const unsigned long long* rows_dev,
                     int64_t add, bool fresh) {
   if (fresh || ctx->status_at != (void*)status || ctx->epoch >= 0xFFFE) {
