@@ -36,13 +36,13 @@ GUIDE_COPY_GBS = 6290.0  # MI355X_MICROARCH.md:36, measured device copy
 # `strong`: --rows / --pids are node totals split over the ranks (c3 = 1e9 rows across the node).
 WORKLOADS = {
     "c3": dict(rows=1e9, partitions=1e6, pids=1e7, zipf=1.1, l0=4, linf=2, public=False, metrics="mean",
-               cpu_sample=6e6, strong=True),  # CPU baseline rows per host core
+               cpu_sample=1.2e7, strong=True),  # CPU baseline rows per host core (~10 s of CPU work)
     # c3v: BASELINE configs[2] as written -- the c3 shape with MEAN + VARIANCE (+ COUNT + SUM): K2 also writes
     # the y slot array and K4 runs a second (y) reduction
     "c3v": dict(rows=1e9, partitions=1e6, pids=1e7, zipf=1.1, l0=4, linf=2, public=False, metrics="variance",
-                cpu_sample=6e6, strong=True),
+                cpu_sample=1.2e7, strong=True),
     "c2": dict(rows=1e8, partitions=1e5, pids=1e6, zipf=0.0, l0=8, linf=4, public=True, metrics="count_sum",
-               cpu_sample=6e6),
+               cpu_sample=1.2e7),
     "c4": dict(rows=5e8, partitions=5e7, pids=1.25e7, zipf=1.1, l0=32, linf=4, public=False, metrics="mean",
                cpu_sample=5e5),  # the oracle's O(P) release dominates at P=5e7
     # c5: UtilityAnalysisEngine.analyze with 64 configurations (L0 x Linf) over 1e8 rows: per-partition
