@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define PDP_ABI_VERSION 2
+#define PDP_ABI_VERSION 3
 
 enum {
   PDP_OK = 0,
@@ -130,6 +130,11 @@ typedef struct pdp_bound_params {
   int32_t reserved;                         /* testing: debug flags (pdp_ctx_set_debug); 0 */
   int32_t flags;                            /* PDP_BOUND_* */
   int32_t reserved2;
+  /* ABI 3: the columns' privacy ids are (id - pid_base): the sampling hashes pid_base + pid (DESIGN.md
+   * 4), so a rank can pass its contiguous range of global ids rebased to [0, num_privacy_ids) -- which
+   * sizes the L0 pre-filter by its own ids -- and get the result of the global ids bit for bit.  0
+   * otherwise. */
+  int64_t pid_base;
 } pdp_bound_params;
 
 /* Dense per-partition accumulators [num_partitions] (device).  row_count is the

@@ -168,6 +168,7 @@ struct KeySpec {
   int pkb;
   uint64_t seed;
   uint64_t num_pids;  // up to 2^32 (pid values 0 .. 2^32 - 1)
+  uint64_t pid_base;  // the sampling hashes pid_base + pid (pdp_bound_params.pid_base)
   uint32_t num_parts;
   uint64_t mult;  // mode 4: bucket digit multiplier (pdp_filter.inc)
   int prof;  // accumulate per-phase s_memtime cycles of k_onesweep (kDebugSweepStamps)
@@ -217,6 +218,7 @@ struct SegParams {
   int k4passes;
   int k4shift[3];
   int k4bits[3];
+  uint64_t pid_base;  // pdp_bound_params.pid_base: the sampling hashes pid_base + pid
   // K4 hot-partition table (pdp_reduce.inc, K4Hot): k4hot != 0 -- the K2 kernel holds a per-block LDS
   // table whose pairs are added in fixed point (q = rint(x * k4q)) and flushed with integer atomics
   // into the accumulators' counts and K4's fixed-point scratch k4glo / k4ghi / k4gfl.
@@ -869,7 +871,7 @@ __device__ __forceinline__ bool onesweep_body(
             ninv += valid && b[k] >= 0;
             r[k].pid = kTagDropped | (d << 22);
           } else {
-            r[k].pid = (d << 22) | ((r[k].pid - s_lo[d]) << 5) | filt_level(filt_prio(ks.seed, r[k].pid, r[k].pk));
+            r[k].pid = (d << 22) | ((r[k].pid - s_lo[d]) << 5) | filt_level(filt_prio(ks.seed, ks.pid_base + r[k].pid, r[k].pk));
           }
         }
       } else {
@@ -1350,11 +1352,12 @@ __global__ void k_stream_starts(const long long* __restrict__ gs_raw_scan, const
 
 // L_inf priorities: R2[i] = {group id, row index, bits(row priority)}.
 __global__ void k_stream_row_prio(const Rec* __restrict__ r, int64_t m, const long long* __restrict__ gsc,
-                                  const long long* __restrict__ gpos, uint64_t seed, Rec* __restrict__ out) {
+                                  const long long* __restrict__ gpos, uint64_t seed, uint64_t base,
+                                  Rec* __restrict__ out) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (int64_t)gridDim.x * blockDim.x) {
     const long long g = gsc[i] - 1;
     const Rec a = r[i];
-    const uint64_t gp = pdp::group_priority(pdp::pid_key(seed, a.pid), a.pk);
+    const uint64_t gp = pdp::group_priority(pdp::pid_key(seed, base + a.pid), a.pk);
     const uint64_t rp = pdp::row_priority(gp, (uint64_t)(i - gpos[g]));
     out[i] = Rec{(uint32_t)g, (uint32_t)i, __longlong_as_double((long long)rp)};
   }
@@ -1363,12 +1366,12 @@ __global__ void k_stream_row_prio(const Rec* __restrict__ r, int64_t m, const lo
 // L0 priorities: R3[g] = {pid ordinal, group id, bits(group priority)}.
 __global__ void k_stream_group_prio(const Rec* __restrict__ r, const long long* __restrict__ psc,
                                     const long long* __restrict__ gpos, int64_t ngroups, uint64_t seed,
-                                    Rec* __restrict__ out) {
+                                    uint64_t base, Rec* __restrict__ out) {
   for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < ngroups;
        g += (int64_t)gridDim.x * blockDim.x) {
     const long long q = gpos[g];
     const Rec a = r[q];
-    const uint64_t gp = pdp::group_priority(pdp::pid_key(seed, a.pid), a.pk);
+    const uint64_t gp = pdp::group_priority(pdp::pid_key(seed, base + a.pid), a.pk);
     out[g] = Rec{(uint32_t)(psc[q] - 1), (uint32_t)g, __longlong_as_double((long long)gp)};
   }
 }
@@ -1922,6 +1925,7 @@ SegParams make_seg(const pdp_bound_params* bp, int low, int pkb, bool has_value)
   sp.low = low;
   sp.pkb = pkb;
   sp.seed = bp->sampling_seed;
+  sp.pid_base = (uint64_t)bp->pid_base;
   sp.l0 = bp->max_partitions_contributed;
   sp.linf = bp->max_contributions_per_partition;
   const int m = bp->metrics;
@@ -2303,7 +2307,8 @@ int run_generic(pdp_ctx* ctx, const Rec* sorted, Rec* spare, Rec* alt, const std
   int32_t* grank;
   HIP_TRY(scratch.alloc((void**)&row_keep, (size_t)total));
   HIP_TRY(scratch.alloc((void**)&grank, (size_t)ngroups * 4));
-  hipLaunchKernelGGL(k_stream_row_prio, dim3(gr), dim3(kThreads), 0, stream, r, total, gsc, gpos, sp.seed, x1);
+  hipLaunchKernelGGL(k_stream_row_prio, dim3(gr), dim3(kThreads), 0, stream, r, total, gsc, gpos, sp.seed, sp.pid_base,
+                     x1);
   Rec* xs = nullptr;
   const int gbits = std::max(1, pdp::ceil_log2_u64((uint64_t)ngroups));
   if ((rc = sort_recs(ctx, x1, x2, total, composite_spec(3, gbits, 64, plan.pkb, U, P), hist, off, counters, status,
@@ -2314,7 +2319,7 @@ int run_generic(pdp_ctx* ctx, const Rec* sorted, Rec* spare, Rec* alt, const std
   // 3) L0 ranks: sort (pid, group priority, group) -> rank within pid.
   const int ggr = grid_for(ngroups, kThreads);
   hipLaunchKernelGGL(k_stream_group_prio, dim3(ggr), dim3(kThreads), 0, stream, r, psc, gpos, (int64_t)ngroups,
-                     sp.seed, x1);
+                     sp.seed, sp.pid_base, x1);
   const int pbits = std::max(1, pdp::ceil_log2_u64((uint64_t)npids));
   if ((rc = sort_recs(ctx, x1, x2, ngroups, composite_spec(3, pbits, 64, plan.pkb, U, P), hist, off, counters,
                       status, status_bytes, ws, stream, &xs)))
@@ -2845,6 +2850,8 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
       return fail(PDP_ERR_INVALID_ARG, "a sweep cannot use contribution_bounds_already_enforced");
     if (b->max_partitions_contributed < 1 || b->max_contributions_per_partition < 1)
       return fail(PDP_ERR_INVALID_ARG, "contribution bounds must be positive");
+    if (b->pid_base < 0 || b->pid_base != bps[0].pid_base)
+      return fail(PDP_ERR_INVALID_ARG, "pid_base must be >= 0 (and the same for every configuration)");
     const bool need_value = (b->metrics & (PDP_METRIC_SUM | PDP_METRIC_MEAN | PDP_METRIC_VARIANCE)) != 0;
     if (need_value && n > 0 && !cols->value)
       return fail(PDP_ERR_INVALID_ARG, "value column required for SUM/MEAN/VARIANCE");
@@ -3017,6 +3024,7 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
   ks.low = plan.low;
   ks.pkb = plan.pkb;
   ks.seed = bp->sampling_seed;
+  ks.pid_base = (uint64_t)bp->pid_base;
   ks.num_pids = (uint64_t)U;
   ks.num_parts = (uint32_t)P;
   ks.passes = plan.passes;

@@ -119,7 +119,11 @@ class World:
         it first, then rank 1's, ...: within a privacy id the concatenated
         input order is kept, so bounding equals one process over the
         concatenated input (pipeline_backend.py:476-485).
-        -> (pid, pk, value, num_privacy_ids)."""
+        -> (pid, pk, value, num_privacy_ids, pid_base): the rank's ids are
+        returned rebased to [0, num_privacy_ids) = its own distinct count, with
+        pid_base = the lower ranks' count, so the library hashes pid_base + pid
+        (BoundConfig.pid_base, ABI 3) -- the global numbering's result -- while
+        sizing the L0 pre-filter by the rank's own ids."""
         import torch
         import torch.distributed as dist
         dest = self.key_owner(h, self.size)
@@ -143,7 +147,7 @@ class World:
         every = [torch.empty_like(mine) for _ in range(self.size)]
         dist.all_gather(every, mine, group=self.group)
         n_each = [int(x.item()) for x in every]
-        return inv.to(torch.int64) + sum(n_each[:self.rank]), pkr, vr, sum(n_each)
+        return inv.to(torch.int64), pkr, vr, n_each[self.rank], sum(n_each[:self.rank])
 
     def reduce_scatter_partials(self, parts, num_partitions: int):
         """Sums the ranks' fixed-point partials (int64, exact) and returns the

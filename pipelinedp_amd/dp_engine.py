@@ -157,16 +157,17 @@ class DPResult:
             value = None
             if need_value:
                 value = torch.as_tensor(col.value).to(device=device, dtype=torch.float64).contiguous()
-            return pid, pk, value, U, P, keys, bool(col.privacy_id_sharded)
+            return pid, pk, value, U, P, keys, bool(col.privacy_id_sharded), 0
         enc = encode_rows(col, self._extractors, public, need_pid=need_pid, need_value=need_value, world=world)
         t = lambda a: torch.from_numpy(a).to(device)  # noqa: E731
         pid, pk, value = (t(enc.pid) if enc.pid is not None else None, t(enc.pk),
                           t(enc.value) if enc.value is not None else None)
-        U, sharded = enc.num_privacy_ids, False
+        U, sharded, base = enc.num_privacy_ids, False, 0
         if enc.pid_hash is not None:  # multi-rank host rows: to the owner of their privacy-id key hash
-            pid, pk, value, U = world.exchange_by_key_hash(t(enc.pid_hash), pk, value)
+            # rank-local ids [0, U) with the global numbering's offset `base` (hashed as base + id)
+            pid, pk, value, U, base = world.exchange_by_key_hash(t(enc.pid_hash), pk, value)
             sharded = True
-        return pid, pk, value, U, len(enc.partition_keys), enc.partition_keys, sharded
+        return pid, pk, value, U, len(enc.partition_keys), enc.partition_keys, sharded, base
 
     def _compute(self):
         backend = self._backend
@@ -187,7 +188,10 @@ class DPResult:
         need_value = bool(mask & (native.METRIC_SUM | native.METRIC_MEAN | native.METRIC_VARIANCE))
         # A World (also of size 1: the RCCL identity, tests/test_gpu_rccl.py) runs the collective path.
         world = backend.world
-        pid, pk, value, U, P, keys, presharded = self._inputs(torch, ex.device, not enforced, need_value, world)
+        pid, pk, value, U, P, keys, presharded, pid_base = self._inputs(torch, ex.device, not enforced, need_value,
+                                                                        world)
+        if pid_base:
+            bounds = dataclasses.replace(bounds, pid_base=pid_base)
         fields = native.metric_fields(mask)
         if world is not None and world.size > 1:
             # every rank must take the same branch below (a rank with P == 0 alone would leave the others

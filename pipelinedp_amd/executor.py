@@ -26,6 +26,9 @@ class BoundConfig:
     sampling_seed: Optional[int] = None
     debug_force_fallback: bool = False
     debug_flags: int = 0
+    # the pid columns hold (privacy id - pid_base); the sampling hashes pid_base + pid (ABI 3): a rank passes
+    # its contiguous range of global ids rebased to [0, U_local) and gets the global ids' result
+    pid_base: int = 0
 
 
 @dataclasses.dataclass
@@ -164,7 +167,7 @@ class HipExecutor:
             int(cfg.min_sum_per_partition is not None),
             float(cfg.min_value or 0.0), float(cfg.max_value or 0.0),
             float(cfg.min_sum_per_partition or 0.0), float(cfg.max_sum_per_partition or 0.0),
-            seed, int(cfg.debug_force_fallback), int(cfg.debug_flags), int(flags), 0)
+            seed, int(cfg.debug_force_fallback), int(cfg.debug_flags), int(flags), 0, int(cfg.pid_base))
 
     def accumulate(self, pid, pk, value, num_privacy_ids: int, num_partitions: int, cfg: BoundConfig,
                    acc: Optional[Accumulators] = None, sync: bool = True) -> Accumulators:

@@ -13,7 +13,7 @@ LIB_PATH = os.environ.get("PDP_HIP_LIB") or os.path.join(_HERE, "libpdp_hip.so")
 PDP_OK = 0
 ERR_OUT_OF_RANGE, ERR_INTERNAL, ERR_NEEDS_SYNC = -4, -5, -6
 BOUND_ASYNC = 1  # pdp_bound_params.flags: no host synchronisation (pdp_get_status afterwards)
-ABI_VERSION = 2
+ABI_VERSION = 3
 METRIC_COUNT, METRIC_SUM, METRIC_MEAN, METRIC_VARIANCE, METRIC_PRIVACY_ID_COUNT = 1, 2, 4, 8, 16
 FIELD_NAMES = {0: "variance", 1: "mean", 2: "count", 3: "sum", 4: "privacy_id_count"}
 NOISE_LAPLACE, NOISE_GAUSSIAN = 0, 1
@@ -53,7 +53,7 @@ class BoundParams(ctypes.Structure):
                 ("min_value", c_f64), ("max_value", c_f64),
                 ("min_sum_per_partition", c_f64), ("max_sum_per_partition", c_f64),
                 ("sampling_seed", c_u64), ("debug_force_fallback", c_i32), ("reserved", c_i32),
-                ("flags", c_i32), ("reserved2", c_i32)]
+                ("flags", c_i32), ("reserved2", c_i32), ("pid_base", c_i64)]
 
 
 class Accumulators(ctypes.Structure):

@@ -52,7 +52,8 @@ class OracleExecutor:
         import torch
 
         from pipelinedp_amd.executor import Partials
-        acc = o.bound_and_accumulate(pid.numpy(), pk.numpy(), value.numpy(), num_partitions, BP, "hash", seed=5)
+        base = int(getattr(bounds, "pid_base", 0) or 0)  # World.aggregate's rebased ids
+        acc = o.bound_and_accumulate(pid.numpy() + base, pk.numpy(), value.numpy(), num_partitions, BP, "hash", seed=5)
         parts = o.k4_partials(acc, num_partitions, BP, MASK)
         fields = Partials.fields_for(MASK)
         data = np.stack([parts[f] for f in fields])

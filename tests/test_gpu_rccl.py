@@ -221,3 +221,41 @@ def test_analysis_of_no_rows():
     assert float(prob.abs().sum()) == 0.0
     assert int(pids.sum()) == 0
     assert float(m.abs().sum()) == 0.0
+
+
+def test_rebased_rank_ids_with_pid_base_equal_global_ids_and_filter():
+    """ABI 3 pid_base: ranks owning contiguous ranges of global privacy ids
+    (the host-rows path, World.exchange_by_key_hash) pass them rebased to
+    [0, U_rank) with pid_base = the range start.  The sampling hashes
+    pid_base + pid, so the merged partials equal one pdp_bound_accumulate over
+    the global ids bit for bit -- and the L0 pre-filter, sized by U_rank, runs on
+    every rank (with the global U it would not: 5e6 rows per rank < 4 L0 U = 6.4e6)."""
+    import dataclasses
+
+    import torch
+    from pipelinedp_amd import native as M
+    from pipelinedp_amd.executor import BoundConfig, HipExecutor, Partials
+    ex = HipExecutor(0)
+    n, P, W = 40_000_000, 100_000, 8  # 5e6 rows per rank: above the filter's 2^22-row minimum
+    U = n // 100
+    pid, pk, val = ex.generate(n, U, P, seed=77, zipf_s=1.1, lo=-2.0, hi=12.0)  # on-device generator
+    cfg = BoundConfig(M.METRIC_COUNT | M.METRIC_SUM | M.METRIC_MEAN | M.METRIC_PRIVACY_ID_COUNT, 4, 2, 0.0, 10.0,
+                      sampling_seed=21)
+    one = ex.accumulate(pid, pk, val, U, P, cfg)
+    torch.cuda.synchronize()
+    bounds = [r * U // W for r in range(W + 1)]
+    total = None
+    for r in range(W):
+        m = (pid >= bounds[r]) & (pid < bounds[r + 1])
+        n_r, U_r = int(m.sum()), bounds[r + 1] - bounds[r]
+        assert (1 << 22) <= n_r < 4 * 4 * U and n_r >= 4 * 4 * U_r  # the filter rule, global U vs rank U
+        rc = dataclasses.replace(cfg, pid_base=bounds[r])
+        parts = ex.accumulate_partials((pid[m] - bounds[r]).contiguous(), pk[m].contiguous(), val[m].contiguous(),
+                                       U_r, P, rc)
+        torch.cuda.synchronize()
+        assert ex.stats().filter_rows > 0, r
+        total = parts.data.clone() if total is None else total + parts.data
+    acc = ex.finalize_partials(Partials(total, parts.fields, P), cfg)
+    torch.cuda.synchronize()
+    assert torch.equal(one.row_count, acc.row_count) and torch.equal(one.count, acc.count)
+    np.testing.assert_array_equal(one.x.cpu().numpy(), acc.x.cpu().numpy())
