@@ -370,8 +370,10 @@ def main():
         mask = native.METRIC_COUNT | native.METRIC_SUM | native.METRIC_PRIVACY_ID_COUNT
         ana_cfgs = [native.AnalysisConfig(l0, linf, SWEEP_SUM_BOUNDS[0], SWEEP_SUM_BOUNDS[1],
                                           native.SELECTION_TRUNCATED_GEOMETRIC, 0, 0.25, 1e-6) for l0, linf in SWEEP]
+    # rank r's privacy ids are global ids r * U + local id: the sampling hashes the global id (pid_base, ABI 3),
+    # so an N-GPU step bounds exactly what one process over the concatenated rows would
     bounds = BoundConfig(mask, args.l0, args.linf, 0.0, 10.0, sampling_seed=args.seed + 1,
-                         debug_flags=args.debug_flags)
+                         debug_flags=args.debug_flags, pid_base=rank * U if world_size > 1 else 0)
     # NaiveBudgetAccountant(eps=1, delta=1e-6): MeanCombiner (Laplace) eps 0.5, selection eps 0.5 delta 1e-6
     eps = [0.0] * 6
     delta = [0.0] * 6
