@@ -397,11 +397,13 @@ def main():
             metrics, prob, pids = ex.analyze(pid, pk, val, U, P, mask, ana_cfgs)
             return (pids > 0,)
         if world is not None:
-            return world.aggregate(ex, pid, pk, val, U, P, bounds, rel, gather=False, sync=False)
+            return world.aggregate_async(ex, pid, pk, val, U, P, bounds, rel, gather=False)
         acc = ex.accumulate(pid, pk, val, U, P, bounds, sync=False)
         return ex.release(acc, rel, bounds)
 
     def check_status():
+        if world is not None and not sweep:
+            world.check_async_status(ex, "cuda")  # every rank's status, before any result is trusted
         if not sweep:
             st_code = ex.status()
             if st_code:

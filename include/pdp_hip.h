@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define PDP_ABI_VERSION 3
+#define PDP_ABI_VERSION 4
 
 enum {
   PDP_OK = 0,
@@ -129,7 +129,7 @@ typedef struct pdp_bound_params {
                                                generic sorted-stream path */
   int32_t reserved;                         /* testing: debug flags (pdp_ctx_set_debug); 0 */
   int32_t flags;                            /* PDP_BOUND_* */
-  int32_t reserved2;
+  int32_t reserved2;                        /* testing: second debug-flag word; 0 */
   /* ABI 3: the columns' privacy ids are (id - pid_base): the sampling hashes pid_base + pid (DESIGN.md
    * 4), so a rank can pass its contiguous range of global ids rebased to [0, num_privacy_ids) -- which
    * sizes the L0 pre-filter by its own ids -- and get the result of the global ids bit for bit.  0
@@ -254,6 +254,13 @@ int pdp_bound_accumulate_sweep(pdp_ctx* ctx, const pdp_columns* cols, const pdp_
  * distributed over ranks. */
 int pdp_release(pdp_ctx* ctx, const pdp_accumulators* acc, int64_t num_partitions, int64_t pk_offset,
                 const pdp_release_params* rp, const pdp_outputs* out, void* stream);
+
+/* Builds (synchronously) the device-side data pdp_release needs for rp -- the truncated-geometric keep
+ * table of (eps, delta, max_partitions_contributed) -- in the context's cache, so that a later
+ * pdp_release on a capturing stream (hipGraph) enqueues kernels only.  Cached tables are immutable and
+ * live until pdp_ctx_destroy: a captured pdp_release stays valid whatever later calls release.
+ * pdp_release under capture without a prepared table returns PDP_ERR_NEEDS_SYNC (ABI 4). */
+int pdp_prepare_release(pdp_ctx* ctx, const pdp_release_params* rp);
 
 /* Field order of MetricsTuple for a metric mask; returns the count. */
 int pdp_metric_fields(int32_t metrics, int32_t* fields_out /* >= 5 */);

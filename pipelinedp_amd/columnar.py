@@ -50,19 +50,24 @@ class EncodedColumns:
     value: Optional[np.ndarray]
     num_privacy_ids: int
     partition_keys: list
-    # multi-rank: the rows' privacy-id key hashes, not yet dense ids -- World.exchange_by_key_hash
+    # multi-rank: the rows' privacy-id key hash pairs [N, 2], not yet dense ids -- World.exchange_by_key_hash
     # moves every row to the rank owning its hash and numbers the privacy ids there
     pid_hash: Optional[np.ndarray] = None
 
 
 def _canon(k) -> bytes:
     """Canonical bytes of a privacy-id key, identical in every process (Python's
-    hash() is salted per process).  Keys equal as dict keys encode equally:
-    numpy scalars as their Python value, integral floats as ints."""
+    hash() is salted per process).  Keys that are equal as dict keys -- the
+    reference groups privacy ids by dict key (pipeline_backend.py:476-485) --
+    encode equally: numpy scalars as their Python value, bools and integral
+    floats as ints (True == 1 == 1.0, False == 0), complex numbers with a zero
+    imaginary part as their real part, tuples element-wise."""
     if isinstance(k, np.generic):
         k = k.item()
+    if isinstance(k, complex) and k.imag == 0:
+        k = k.real
     if isinstance(k, bool):
-        return b"b1" if k else b"b0"
+        k = int(k)
     if isinstance(k, float) and k.is_integer():
         k = int(k)
     if isinstance(k, int):
@@ -80,24 +85,74 @@ def _canon(k) -> bytes:
     return b"r" + repr(k).encode()
 
 
-def key_hashes(keys) -> np.ndarray:
-    """64-bit hash (int64) of each key: blake2b of its canonical bytes."""
+def _digest_words(canon: bytes):
     import hashlib
-    out = np.empty(len(keys), dtype=np.int64)
+    d = hashlib.blake2b(canon, digest_size=16).digest()
+    return int.from_bytes(d[:8], "little", signed=True), int.from_bytes(d[8:], "little", signed=True)
+
+
+def key_hashes(keys) -> np.ndarray:
+    """128-bit hash of each key as two int64 words [len(keys), 2]: the
+    blake2b-128 digest of its canonical bytes (``_canon``).  Word 0 picks the
+    owning rank (distributed.World.key_owner); the pair orders the dense ids."""
+    out = np.empty((len(keys), 2), dtype=np.int64)
     for i, k in enumerate(keys):
-        out[i] = int.from_bytes(hashlib.blake2b(_canon(k), digest_size=8).digest(), "little", signed=True)
+        out[i] = _digest_words(_canon(k))
     return out
 
 
+def _pair_order(h):
+    """Row order of an [M, 2] int64 array sorted by (word 0, word 1), signed."""
+    h = np.asarray(h, dtype=np.int64).reshape(-1, 2)
+    return np.lexsort((h[:, 1], h[:, 0]))
+
+
 def dense_ids_from_hashes(h):
-    """Privacy ids numbered by the ascending (signed) order of their key hash:
-    the numbering World.exchange_by_key_hash reproduces across ranks without
-    exchanging keys (ranks own contiguous hash ranges).  Distinct keys with
-    equal 64-bit hashes (probability ~U^2 / 2^65) share one privacy id: their
-    contributions are bounded together -- stricter bounding, never weaker
-    privacy."""
-    uniq, inv = np.unique(np.asarray(h, dtype=np.int64), return_inverse=True)
-    return inv.astype(np.int64).reshape(-1), len(uniq)
+    """Dense privacy ids numbered by the ascending (signed) order of the
+    128-bit key hash pairs [N, 2]: the numbering World.exchange_by_key_hash
+    reproduces across ranks without exchanging keys (ranks own contiguous
+    ranges of word 0).  -> (ids [N], number of distinct pairs)."""
+    h = np.asarray(h, dtype=np.int64).reshape(-1, 2)
+    if not len(h):
+        return np.zeros(0, np.int64), 0
+    o = _pair_order(h)
+    hs = h[o]
+    new = np.ones(len(h), dtype=bool)
+    new[1:] = (hs[1:, 0] != hs[:-1, 0]) | (hs[1:, 1] != hs[:-1, 1])
+    ids = np.empty(len(h), np.int64)
+    ids[o] = np.cumsum(new) - 1
+    return ids, int(new.sum())
+
+
+def dense_ids_exact(uniq_keys, hashes):
+    """Dense ids of distinct keys (``uniq_keys``: one per dict-equality class,
+    as pandas.factorize yields them) in the order of their hash pairs, with
+    EXACT handling of collisions: keys whose 128-bit hashes are equal are told
+    apart by their canonical bytes (then by first appearance), so distinct
+    keys always get distinct ids and equal keys one id -- the reference's
+    dict grouping (pipeline_backend.py:476-485).  Without a collision the
+    numbering is dense_ids_from_hashes'.  -> ids [M]."""
+    M = len(uniq_keys)
+    h = np.asarray(hashes, dtype=np.int64).reshape(-1, 2)
+    o = _pair_order(h)
+    hs = h[o]
+    same = np.zeros(M, dtype=bool)
+    if M > 1:
+        same[1:] = (hs[1:, 0] == hs[:-1, 0]) & (hs[1:, 1] == hs[:-1, 1])
+    if same.any():  # runs of equal hash pairs: order each run by (canonical bytes, first appearance)
+        o = o.copy()
+        i = 0
+        while i < M:
+            j = i + 1
+            while j < M and same[j]:
+                j += 1
+            if j - i > 1:
+                run = o[i:j]
+                o[i:j] = sorted(run, key=lambda r: (_canon(uniq_keys[r]), r))
+            i = j
+    ids = np.empty(M, np.int64)
+    ids[o] = np.arange(M, dtype=np.int64)
+    return ids
 
 
 def _factorize(values):
@@ -147,13 +202,17 @@ def encode_rows(rows, extractors, public_partitions=None, need_pid=True, need_va
     (``_global_keys``: dense partition ids mean the same key on every rank,
     which the reduce-scatter of [P] partials needs).
 
-    Privacy ids are numbered by their key hash (``dense_ids_from_hashes``),
-    in one process and across ranks alike, so the sampling (keyed by the
-    dense id) is the same whatever the world size.  With a multi-rank world
-    no privacy-id key leaves its rank: the rows carry their key hashes
-    (``pid_hash``), and ``World.exchange_by_key_hash`` moves them to the rank
-    owning the hash (the reference's group-by-privacy-id shuffle,
-    pipeline_backend.py:476-485) and numbers them there.
+    Privacy ids are grouped by dict equality, as the reference groups them
+    (pipeline_backend.py:476-485: ``True``, ``1`` and ``1.0`` are one id), and
+    numbered by their 128-bit key hash, in one process and across ranks
+    alike, so the sampling (keyed by the dense id) is the same whatever the
+    world size.  In one process the numbering is exact (``dense_ids_exact``:
+    colliding hashes are told apart by the keys).  With a multi-rank world no
+    privacy-id key leaves its rank: the rows carry their key hash pairs
+    (``pid_hash`` [N, 2]), and ``World.exchange_by_key_hash`` moves them to the
+    rank owning the hash (the reference's group-by-privacy-id shuffle) and
+    numbers the distinct pairs there; only a full 128-bit collision of two
+    distinct keys (probability ~U^2 / 2^129) would merge them.
     """
     rows = rows if isinstance(rows, list) else list(rows)
     multi = world is not None and world.size > 1
@@ -170,14 +229,14 @@ def encode_rows(rows, extractors, public_partitions=None, need_pid=True, need_va
     if need_pid:
         pid_raw = [extractors.privacy_id_extractor(r) for r in rows]
         if rows:
-            codes, uniq = _factorize(pid_raw)  # hash each distinct key once
-            h = key_hashes(uniq)[codes]
+            codes, uniq = _factorize(pid_raw)  # dict-equal keys share a code; hash each distinct key once
+            hu = key_hashes(uniq)
         else:
-            h = np.zeros(0, np.int64)
+            codes, uniq, hu = np.zeros(0, np.int64), [], np.zeros((0, 2), np.int64)
         if multi:
-            pid_hash = h
+            pid_hash = hu[codes]
         else:
-            pid, U = dense_ids_from_hashes(h)
+            pid, U = dense_ids_exact(uniq, hu)[codes], len(uniq)
     value = None
     if need_value:
         value = np.asarray([extractors.value_extractor(r) for r in rows], dtype=np.float64)

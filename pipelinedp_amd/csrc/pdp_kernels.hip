@@ -266,6 +266,8 @@ constexpr int kDebugAnaFlags = 128;         // utility analysis: round-3 per-row
 constexpr int kDebugAnaSelLds = 256;        // utility analysis: round-3 per-regime selection kernels
 constexpr int kDebugDevOcc2 = 512;          // device-sized look-back passes at 2 blocks per CU (no spills, slower)
 constexpr int kDebugK4Compact = 1024;       // K2 writes compacted K4 pair records (k4_claim) instead of a slot per row
+// Second word of testing flags (pdp_bound_params.reserved2; the first word's 31 bits are taken).
+constexpr int kDebug2OverflowFull1 = 1;     // a second overflow range already sets kCtrFull (the whole-input redo)
 // Timing ablations whose results are invalid: accepted only by a -DPDP_DEBUG_BUILD library.
 constexpr int kAblationFlags = kDebugSortOnly | kDebugNoLookback | kDebugLinearWrite | kDebugNoScatter |
                                kDebugNoAtomics | kDebugWalkOnly | kDebugNoLinf | kDebugNoSums | kDebugFilterTiming;
@@ -285,6 +287,9 @@ struct AccPtrs {
 struct OvList {
   unsigned long long* ranges;  // [cap][2] (start, end)
   unsigned long long* counters;
+  // testing (debug2 flag OVERFLOW_FULL1): more than this many overflow ranges also set kCtrFull (the ranges
+  // stay recorded and valid); 0 = only beyond kOverflowCap
+  unsigned long long full_at;
 };
 
 // Digit of radix pass `pass` of record r.  Mode 3 sorts by the 96-bit key
@@ -1200,6 +1205,10 @@ __global__ __launch_bounds__(kThreads) void k_zero64(unsigned long long* __restr
   for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < words; i += (int64_t)gridDim.x * kThreads)
     p[i] = 0ull;
 }
+__global__ __launch_bounds__(kThreads) void k_zero_bytes(unsigned char* __restrict__ p, int64_t bytes) {
+  for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < bytes; i += (int64_t)gridDim.x * kThreads)
+    p[i] = 0u;
+}
 
 // End of a pdp_bound_accumulate call: the counters the host needs (errors, the generic-path request,
 // statistics) -> the context's device status block (kStat*), read back by ONE copy (or, for an
@@ -1233,9 +1242,8 @@ __device__ __forceinline__ void record_overflow(const OvList& ov, int64_t s, int
   if (i < kOverflowCap) {
     ov.ranges[2 * i] = (unsigned long long)s;
     ov.ranges[2 * i + 1] = (unsigned long long)e;
-  } else {
-    atomicOr(&ov.counters[kCtrFull], 1ull);
   }
+  if (i >= kOverflowCap || (ov.full_at && i >= ov.full_at)) atomicOr(&ov.counters[kCtrFull], 1ull);
 }
 
 __device__ __forceinline__ void row_terms(const SegParams& sp, double v, double& x, double& y) {
@@ -1852,10 +1860,15 @@ int grid_for(int64_t n, int threads, int cap = 4096) {
   return (int)g;
 }
 
-// hipMemsetAsync(p, 0, bytes) as a kernel (k_zero64): p 8-byte aligned, bytes a multiple of 8.
+// hipMemsetAsync(p, 0, bytes) as a kernel, so a captured call holds kernel nodes only: k_zero64 for
+// 8-byte aligned buffers of whole words, k_zero_bytes otherwise (no hipMemsetAsync fallback).
 hipError_t zero_async(void* p, size_t bytes, hipStream_t stream) {
   if (bytes == 0) return hipSuccess;
-  if (((uintptr_t)p & 7u) || (bytes & 7u)) return hipMemsetAsync(p, 0, bytes, stream);
+  if (((uintptr_t)p & 7u) || (bytes & 7u)) {
+    hipLaunchKernelGGL(k_zero_bytes, dim3(grid_for((int64_t)bytes, kThreads, 1024)), dim3(kThreads), 0, stream,
+                       (unsigned char*)p, (int64_t)bytes);
+    return hipGetLastError();
+  }
   const int64_t words = (int64_t)(bytes / 8);
   hipLaunchKernelGGL(k_zero64, dim3(grid_for(words, kThreads, 4096)), dim3(kThreads), 0, stream,
                      (unsigned long long*)p, words);
@@ -1976,11 +1989,18 @@ struct pdp_ctx {
   size_t status_ok = 0;  // bytes of the look-back status region cleared for the current epoch run
   uint32_t epoch = 0;
   pdp_stats stats{};
-  std::vector<double> table_host;
-  double* table_dev = nullptr;
-  size_t table_cap = 0;
-  double table_key[3] = {-1, -1, -1};
-  int64_t table_len = 0;
+  // Truncated-geometric keep tables, one per (eps, delta, L0), built outside any stream capture
+  // (selection_table / pdp_prepare_release) and immutable until pdp_ctx_destroy: a hipGraph that captured
+  // pdp_release keeps their device pointer.  (Round 5 rewrote one table in place, or freed it for a
+  // larger one: a graph captured earlier then replayed the wrong keep probabilities or a dangling
+  // pointer.)
+  struct SelTable {
+    double eps, delta;
+    int64_t k;
+    double* dev;
+    int64_t len;
+  };
+  std::vector<SelTable> tables;
 };
 
 namespace {
@@ -2408,6 +2428,47 @@ int decode_status(pdp_ctx* ctx, const unsigned long long* h);
 
 }  // namespace
 
+namespace {
+
+// The truncated-geometric keep table of (eps, delta, k) on the device: found in the context's immutable
+// cache, or built there.  Building needs a host copy and an allocation, which a stream capture must not
+// contain: under capture an uncached table is PDP_ERR_NEEDS_SYNC (call pdp_prepare_release first).
+int selection_table(pdp_ctx* ctx, double eps, double delta, int64_t k, hipStream_t stream, const double** dev,
+                    int64_t* len) {
+  for (const auto& t : ctx->tables) {
+    if (t.eps == eps && t.delta == delta && t.k == k) {
+      *dev = t.dev;
+      *len = t.len;
+      return 0;
+    }
+  }
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  HIP_TRY(hipStreamIsCapturing(stream, &cs));
+  if (cs != hipStreamCaptureStatusNone)
+    return fail(PDP_ERR_NEEDS_SYNC, "pdp_release under stream capture needs its selection table prepared first "
+                                    "(pdp_prepare_release before the capture)");
+  int64_t n = 0;
+  if (int rc = pdp_truncated_geometric_table(eps, delta, k, nullptr, 0, &n)) return rc;
+  std::vector<double> host((size_t)n, 0.0);
+  int64_t n2 = 0;
+  if (int rc = pdp_truncated_geometric_table(eps, delta, k, host.data(), n, &n2)) return rc;
+  double* d = nullptr;
+  HIP_TRY(hipMalloc((void**)&d, (size_t)std::max<int64_t>(n, 1) * 8));
+  if (n > 0) {
+    const hipError_t e = hipMemcpy(d, host.data(), (size_t)n * 8, hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+      (void)hipFree(d);
+      return fail(PDP_ERR_HIP, std::string("selection table copy: ") + hipGetErrorString(e));
+    }
+  }
+  ctx->tables.push_back({eps, delta, k, d, n});
+  *dev = d;
+  *len = n;
+  return 0;
+}
+
+}  // namespace
+
 extern "C" {
 
 int pdp_abi_version(void) { return PDP_ABI_VERSION; }
@@ -2429,7 +2490,7 @@ void pdp_ctx_destroy(pdp_ctx* ctx) {
     (void)hipEventDestroy(r.b);
   }
   for (auto e : ctx->pool) (void)hipEventDestroy(e);
-  if (ctx->table_dev) (void)hipFree(ctx->table_dev);
+  for (auto& t : ctx->tables) (void)hipFree(t.dev);
   if (ctx->dstat) (void)hipFree(ctx->dstat);
   delete ctx;
 }
@@ -3152,7 +3213,7 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
     n_slot = kCtrNGeneric;
   }
 
-  OvList ov{ranges, counters};
+  OvList ov{ranges, counters, (bp->reserved2 & kDebug2OverflowFull1) ? 1ull : 0ull};
   BigList big{(unsigned long long*)(ws + L.big), L.big_cap};
   const int64_t seg_grid = (n + kSegTile - 1) / kSegTile;
   Rec* alt = sweep ? (Rec*)(ws + L.recs_c) : sorted;
@@ -3287,6 +3348,15 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
     if (k4.on) {
       HIP_TRY(zero_async(k4rep, (size_t)kK4Rep * kK4MaxPasses * 256 * 4, stream));  // drop K2's records
       k4_slots = 0;
+      if (sp.k4hot) {
+        // K2's hot-partition tables already flushed their kept groups: counts into the accumulators, sums
+        // into K4's fixed-point scratch (which k4_finish re-emits through krx.addg).  The generic path
+        // redoes every row, so drop them too, or those groups count twice (round-5 advisor finding).
+        HIP_TRY(zero_async(acc.row_count, (size_t)P * 8, stream));
+        if (acc.count) HIP_TRY(zero_async(acc.count, (size_t)P * 8, stream));
+        HIP_TRY(zero_async(k4lo, (size_t)P * 16, stream));  // lo, hi
+        HIP_TRY(zero_async(k4fl, ((size_t)P * 4 + 7) / 8 * 8, stream));
+      }
     } else {
       HIP_TRY(zero_async(acc.row_count, (size_t)P * 8, stream));
       if (acc.count) HIP_TRY(zero_async(acc.count, (size_t)P * 8, stream));
@@ -3824,27 +3894,7 @@ int pdp_release(pdp_ctx* ctx, const pdp_accumulators* accp, int64_t P, int64_t p
   if (rp->selection != PDP_SELECTION_NONE) {
     const double se = rp->eps[PDP_MECH_SELECTION], sd = rp->delta[PDP_MECH_SELECTION];
     if (rp->selection == PDP_SELECTION_TRUNCATED_GEOMETRIC) {
-      if (!(ctx->table_key[0] == se && ctx->table_key[1] == sd && ctx->table_key[2] == l0 && ctx->table_dev)) {
-        int64_t len = 0;
-        if (int rc = pdp_truncated_geometric_table(se, sd, rp->max_partitions_contributed, nullptr, 0, &len)) return rc;
-        ctx->table_host.assign((size_t)len, 0.0);
-        int64_t len2 = 0;
-        pdp_truncated_geometric_table(se, sd, rp->max_partitions_contributed, ctx->table_host.data(), len, &len2);
-        if ((size_t)len > ctx->table_cap) {
-          if (ctx->table_dev) HIP_TRY(hipFree(ctx->table_dev));
-          ctx->table_dev = nullptr;
-          HIP_TRY(hipMalloc((void**)&ctx->table_dev, (size_t)len * 8));
-          ctx->table_cap = (size_t)len;
-        }
-        HIP_TRY(hipMemcpyAsync(ctx->table_dev, ctx->table_host.data(), (size_t)len * 8, hipMemcpyHostToDevice, stream));
-        HIP_TRY(hipStreamSynchronize(stream));
-        ctx->table_len = len;
-        ctx->table_key[0] = se;
-        ctx->table_key[1] = sd;
-        ctx->table_key[2] = l0;
-      }
-      q.table = ctx->table_dev;
-      q.tlen = ctx->table_len;
+      if (int rc = selection_table(ctx, se, sd, rp->max_partitions_contributed, stream, &q.table, &q.tlen)) return rc;
     } else if (rp->selection == PDP_SELECTION_LAPLACE_THRESHOLDING ||
                rp->selection == PDP_SELECTION_GAUSSIAN_THRESHOLDING) {
       if (int rc = pdp_selection_threshold(rp->selection, se, sd, rp->max_partitions_contributed, &q.sel_thr,
@@ -3861,6 +3911,17 @@ int pdp_release(pdp_ctx* ctx, const pdp_accumulators* accp, int64_t P, int64_t p
                      accp->y, P, pk_offset, q, out->keep, out->metrics);
   HIP_TRY(hipGetLastError());
   return 0;
+}
+
+int pdp_prepare_release(pdp_ctx* ctx, const pdp_release_params* rp) {
+  if (!ctx || !rp) return fail(PDP_ERR_INVALID_ARG, "null argument");
+  if (rp->selection != PDP_SELECTION_TRUNCATED_GEOMETRIC) return 0;
+  DeviceGuard dg(ctx->device);
+  if (!dg.ok) return fail(PDP_ERR_HIP, "hipSetDevice failed");
+  const double* dev = nullptr;
+  int64_t len = 0;
+  return selection_table(ctx, rp->eps[PDP_MECH_SELECTION], rp->delta[PDP_MECH_SELECTION],
+                         rp->max_partitions_contributed, nullptr, &dev, &len);
 }
 
 int pdp_profile_enable(pdp_ctx* ctx, int enable) {

@@ -104,21 +104,25 @@ class World:
 
     @staticmethod
     def key_owner(h, size: int):
-        """Rank owning a privacy-id key hash (int64 tensor): ranks own
-        contiguous ranges of the signed hash order, rank 0 the lowest."""
+        """Rank owning a privacy-id key hash (int64 tensor of hash word 0):
+        ranks own contiguous ranges of the signed hash order, rank 0 the
+        lowest."""
         hi = ((h >> 32) & 0xFFFFFFFF) ^ 0x80000000
         return (hi * size) >> 32
 
     def exchange_by_key_hash(self, h, pk, value):
         """Rows of host-encoded input (columnar.encode_rows with a world) ->
-        the rank owning their privacy-id key hash, then dense privacy ids there:
-        the rank's distinct hashes in ascending order, offset by the distinct
-        counts of the lower ranks (one all-gather of one integer).  No key
-        crosses a rank.  The numbering equals one process's
-        (columnar.dense_ids_from_hashes), and rank r receives rank 0's rows for
-        it first, then rank 1's, ...: within a privacy id the concatenated
-        input order is kept, so bounding equals one process over the
-        concatenated input (pipeline_backend.py:476-485).
+        the rank owning their privacy-id key hash, then dense privacy ids there.
+        ``h`` is the rows' [N, 2] int64 hash pairs (columnar.key_hashes); word 0
+        picks the owner, and the owner numbers its distinct PAIRS in ascending
+        (word 0, word 1) order, offset by the distinct counts of the lower ranks
+        (one all-gather of one integer): two keys that share word 0 but not
+        word 1 stay two privacy ids.  No key crosses a rank.  The numbering
+        equals one process's (columnar.dense_ids_from_hashes /
+        dense_ids_exact), and rank r receives rank 0's rows for it first, then
+        rank 1's, ...: within a privacy id the concatenated input order is
+        kept, so bounding equals one process over the concatenated input
+        (pipeline_backend.py:476-485).
         -> (pid, pk, value, num_privacy_ids, pid_base): the rank's ids are
         returned rebased to [0, num_privacy_ids) = its own distinct count, with
         pid_base = the lower ranks' count, so the library hashes pid_base + pid
@@ -126,7 +130,8 @@ class World:
         sizing the L0 pre-filter by the rank's own ids."""
         import torch
         import torch.distributed as dist
-        dest = self.key_owner(h, self.size)
+        h = h.reshape(-1, 2)
+        dest = self.key_owner(h[:, 0], self.size)
         order = torch.argsort(dest, stable=True)
         counts = torch.bincount(dest, minlength=self.size).to(torch.int64)
         recv = torch.empty_like(counts)
@@ -141,13 +146,20 @@ class World:
             dist.all_to_all_single(out, t[order].contiguous(), out_splits, in_splits, group=self.group)
             return out
 
-        hr, pkr, vr = move(h), move(pk), move(value)
-        uniq, inv = torch.unique(hr, sorted=True, return_inverse=True)
-        mine = torch.tensor([uniq.numel()], dtype=torch.int64, device=h.device)
+        h0, h1, pkr, vr = move(h[:, 0]), move(h[:, 1]), move(pk), move(value)
+        # ids = rank of (h0, h1) among the distinct received pairs: lexicographic order by two stable sorts
+        o = torch.argsort(h1, stable=True)
+        o = o[torch.argsort(h0[o], stable=True)]
+        new = torch.ones(total, dtype=torch.bool, device=h.device)
+        if total > 1:
+            new[1:] = (h0[o][1:] != h0[o][:-1]) | (h1[o][1:] != h1[o][:-1])
+        ids = torch.empty(total, dtype=torch.int64, device=h.device)
+        ids[o] = torch.cumsum(new.to(torch.int64), 0) - 1
+        mine = torch.tensor([int(new.sum().item()) if total else 0], dtype=torch.int64, device=h.device)
         every = [torch.empty_like(mine) for _ in range(self.size)]
         dist.all_gather(every, mine, group=self.group)
         n_each = [int(x.item()) for x in every]
-        return inv.to(torch.int64), pkr, vr, n_each[self.rank], sum(n_each[:self.rank])
+        return ids, pkr, vr, n_each[self.rank], sum(n_each[:self.rank])
 
     def reduce_scatter_partials(self, parts, num_partitions: int):
         """Sums the ranks' fixed-point partials (int64, exact) and returns the
@@ -174,15 +186,47 @@ class World:
         return Partials(dst, parts.fields, b)
 
     def aggregate(self, ex, pid, pk, value, num_privacy_ids, num_partitions, bounds, rel, gather=True,
-                  shuffle=False, sync=True):
+                  shuffle=False):
         """Rank-local bound+accumulate, reduce-scatter, owner-side release.
 
         ``shuffle``: first move every row to rank shard_of(pid)
         (``shuffle_by_privacy_id``); without it the rows must already be
-        sharded by privacy id.  ``sync=False``: the rank-local accumulate does
-        not wait for the stream (check ``ex.status()`` after it drained).  Returns (keep [P], metrics [F, P], fields) of
+        sharded by privacy id.  Returns (keep [P], metrics [F, P], fields) of
         ALL partitions on every rank when ``gather`` (all-gather of the owned
-        blocks), else of the owned block only."""
+        blocks), else of the owned block only.  The rank-local accumulate is
+        synchronous: its partials are complete before they are reduce-scattered
+        and released (an input that needs the generic path is finished)."""
+        return self._aggregate(ex, pid, pk, value, num_privacy_ids, num_partitions, bounds, rel, gather, shuffle,
+                               True)
+
+    def aggregate_async(self, ex, pid, pk, value, num_privacy_ids, num_partitions, bounds, rel, gather=False):
+        """Benchmark / graph-capture form of ``aggregate`` (rows already sharded
+        by privacy id): the rank-local accumulate does not wait for its stream,
+        so the reduce-scatter and release are enqueued before any rank knows
+        whether its input needed the generic path.  The outputs are valid only
+        after ``check_async_status(ex)`` returned on every rank once the
+        streams drained; it raises (on every rank) when one rank reported
+        ERR_NEEDS_SYNC or an error -- then run ``aggregate`` instead.  Not part
+        of the DPEngine path."""
+        return self._aggregate(ex, pid, pk, value, num_privacy_ids, num_partitions, bounds, rel, gather, False,
+                               False)
+
+    def check_async_status(self, ex, device=None):
+        """All ranks' ``ex.status()`` after ``aggregate_async`` (streams drained):
+        raises native.NativeError everywhere if any rank's is not 0."""
+        import torch
+        import torch.distributed as dist
+
+        from . import native
+        st = int(ex.status())
+        t = torch.tensor([-st], dtype=torch.int64, device=device)  # codes are <= 0: MAX of the negation
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+        worst = -int(t.item())
+        if worst != 0:
+            raise native.NativeError(f"aggregate_async: a rank's accumulate returned {worst} "
+                                     "(ERR_NEEDS_SYNC: its input needs the generic path; use aggregate())")
+
+    def _aggregate(self, ex, pid, pk, value, num_privacy_ids, num_partitions, bounds, rel, gather, shuffle, sync):
         import torch
         import torch.distributed as dist
         if shuffle and pid is not None:

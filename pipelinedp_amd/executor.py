@@ -26,6 +26,7 @@ class BoundConfig:
     sampling_seed: Optional[int] = None
     debug_force_fallback: bool = False
     debug_flags: int = 0
+    debug_flags2: int = 0  # pdp_bound_params.reserved2 (testing: DEBUG2_* in native.py)
     # the pid columns hold (privacy id - pid_base); the sampling hashes pid_base + pid (ABI 3): a rank passes
     # its contiguous range of global ids rebased to [0, U_local) and gets the global ids' result
     pid_base: int = 0
@@ -167,7 +168,8 @@ class HipExecutor:
             int(cfg.min_sum_per_partition is not None),
             float(cfg.min_value or 0.0), float(cfg.max_value or 0.0),
             float(cfg.min_sum_per_partition or 0.0), float(cfg.max_sum_per_partition or 0.0),
-            seed, int(cfg.debug_force_fallback), int(cfg.debug_flags), int(flags), 0, int(cfg.pid_base))
+            seed, int(cfg.debug_force_fallback), int(cfg.debug_flags), int(flags), int(cfg.debug_flags2),
+            int(cfg.pid_base))
 
     def accumulate(self, pid, pk, value, num_privacy_ids: int, num_partitions: int, cfg: BoundConfig,
                    acc: Optional[Accumulators] = None, sync: bool = True) -> Accumulators:
@@ -248,23 +250,35 @@ class HipExecutor:
                      "pdp_bound_accumulate_sweep")
         return out
 
-    def release(self, acc: Accumulators, cfg: ReleaseConfig, bounds: BoundConfig, pk_offset: int = 0,
-                num_partitions: Optional[int] = None, offset_in_acc: int = 0):
-        """pdp_release -> (keep uint8 [P], metrics float64 [F, P], field names)."""
-        torch = self.torch
-        P = acc.num_partitions if num_partitions is None else int(num_partitions)
-        fields = native.metric_fields(cfg.metrics_mask)
-        keep = torch.empty(max(P, 1), dtype=torch.uint8, device=self.device)
-        out = torch.empty((max(len(fields), 1), max(P, 1)), dtype=torch.float64, device=self.device)
+    @staticmethod
+    def _release_params(cfg: ReleaseConfig, bounds: BoundConfig):
         eps = (ctypes.c_double * native.NUM_MECH)(*cfg.eps)
         delta = (ctypes.c_double * native.NUM_MECH)(*cfg.delta)
         seed = cfg.noise_seed if cfg.noise_seed is not None else secrets.randbits(64)
-        rp = native.ReleaseParams(
+        return native.ReleaseParams(
             cfg.metrics_mask, cfg.noise_kind, cfg.selection, int(cfg.add_noise), bounds.max_partitions_contributed,
             bounds.max_contributions_per_partition, int(bounds.min_value is not None),
             int(bounds.min_sum_per_partition is not None), float(bounds.min_value or 0.0),
             float(bounds.max_value or 0.0), float(bounds.min_sum_per_partition or 0.0),
             float(bounds.max_sum_per_partition or 0.0), eps, delta, int(cfg.max_rows_per_privacy_id), seed)
+
+    def prepare_release(self, cfg: ReleaseConfig, bounds: BoundConfig):
+        """pdp_prepare_release: build release's device-side table (truncated
+        geometric selection) now, outside any stream capture, so that a
+        release() captured in a CUDA/HIP graph enqueues kernels only."""
+        rp = self._release_params(cfg, bounds)
+        native.check(self.lib.pdp_prepare_release(self.ctx, ctypes.byref(rp)), "pdp_prepare_release")
+
+    def release(self, acc: Accumulators, cfg: ReleaseConfig, bounds: BoundConfig, pk_offset: int = 0,
+                num_partitions: Optional[int] = None, offset_in_acc: int = 0):
+        """pdp_release -> (keep uint8 [P], metrics float64 [F, P], field names).
+        Under stream capture call prepare_release() first (else NEEDS_SYNC)."""
+        torch = self.torch
+        P = acc.num_partitions if num_partitions is None else int(num_partitions)
+        fields = native.metric_fields(cfg.metrics_mask)
+        keep = torch.empty(max(P, 1), dtype=torch.uint8, device=self.device)
+        out = torch.empty((max(len(fields), 1), max(P, 1)), dtype=torch.float64, device=self.device)
+        rp = self._release_params(cfg, bounds)
         outs = native.Outputs(ctypes.c_void_p(keep.data_ptr()), ctypes.c_void_p(out.data_ptr()))
         accs = acc.as_struct(offset_in_acc)
         native.check(self.lib.pdp_release(self.ctx, ctypes.byref(accs), P, int(pk_offset), ctypes.byref(rp),

@@ -13,7 +13,7 @@ LIB_PATH = os.environ.get("PDP_HIP_LIB") or os.path.join(_HERE, "libpdp_hip.so")
 PDP_OK = 0
 ERR_OUT_OF_RANGE, ERR_INTERNAL, ERR_NEEDS_SYNC = -4, -5, -6
 BOUND_ASYNC = 1  # pdp_bound_params.flags: no host synchronisation (pdp_get_status afterwards)
-ABI_VERSION = 3
+ABI_VERSION = 4
 METRIC_COUNT, METRIC_SUM, METRIC_MEAN, METRIC_VARIANCE, METRIC_PRIVACY_ID_COUNT = 1, 2, 4, 8, 16
 FIELD_NAMES = {0: "variance", 1: "mean", 2: "count", 3: "sum", 4: "privacy_id_count"}
 NOISE_LAPLACE, NOISE_GAUSSIAN = 0, 1
@@ -35,6 +35,8 @@ DEBUG_ANA_SEL_LDS = 256
 DEBUG_DEV_OCC2 = 512  # device-sized look-back passes at 2 blocks per CU
 DEBUG_K4_COMPACT = 1024  # K2 claims compacted K4 pair slots (one atomic counter; measured slower)
 DEBUG_THIN2 = 67108864  # K4 on: the LDS-staged k_thin2 instead of k_thin (measured slower)
+# second flag word (pdp_bound_params.reserved2)
+DEBUG2_OVERFLOW_FULL1 = 1  # a second overflow range already sets the "redo everything on the generic path" flag
 DEBUG_NO_HOT_CACHE = 524288  # K2 without its hot-partition table (K4 off: LDS atomics cache; K4 on: K4Hot)
 
 c_i32, c_i64, c_u64, c_f64 = ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64, ctypes.c_double
@@ -130,6 +132,7 @@ SIGNATURES = [
                                            ctypes.POINTER(Accumulators), c_vp, ctypes.c_size_t, c_vp]),
     ("pdp_release", c_i32, [c_vp, ctypes.POINTER(Accumulators), c_i64, c_i64, ctypes.POINTER(ReleaseParams),
                             ctypes.POINTER(Outputs), c_vp]),
+    ("pdp_prepare_release", c_i32, [c_vp, ctypes.POINTER(ReleaseParams)]),
     ("pdp_metric_fields", c_i32, [c_i32, ctypes.POINTER(c_i32)]),
     ("pdp_gaussian_sigma", c_f64, [c_f64, c_f64, c_f64]),
     ("pdp_truncated_geometric_table", c_i32, [c_f64, c_f64, c_i64, ctypes.POINTER(c_f64), c_i64,

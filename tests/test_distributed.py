@@ -323,6 +323,74 @@ def test_many_privacy_ids_two_ranks_no_key_exchange_bitwise(tmp_path):
     assert sum(acc_rows) == len(rows)
 
 
+# --- privacy-id hash collisions across ranks -----------------------------------
+# Word 0 of every key hash (the owning rank) keeps only its top 2 bits, so most
+# privacy ids share word 0 with others on their rank; the owner must still tell
+# them apart by word 1 (World.exchange_by_key_hash numbers distinct PAIRS).
+# Bitwise equal to one process under the same patch.
+
+
+def _collide_hashes(keys):
+    from pipelinedp_amd import columnar
+    h = columnar._real_key_hashes(keys)
+    h[:, 0] = (h[:, 0] >> 62) << 62
+    return h
+
+
+def _patch_hashes():
+    from pipelinedp_amd import columnar
+    if not hasattr(columnar, "_real_key_hashes"):
+        columnar._real_key_hashes = columnar.key_hashes
+    columnar.key_hashes = _collide_hashes
+
+
+def _unpatch_hashes():
+    from pipelinedp_amd import columnar
+    if hasattr(columnar, "_real_key_hashes"):
+        columnar.key_hashes = columnar._real_key_hashes
+
+
+def _collide_worker(rank, world_size, port, outdir):
+    import json
+
+    import torch.distributed as dist
+
+    from pipelinedp_amd.distributed import World
+    _patch_hashes()
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world_size)
+    try:
+        rows = _engine_rows()[rank::world_size]
+        out, _ = _run_engine(rows, World(rank, world_size))
+        with open(os.path.join(outdir, f"collide{rank}.json"), "w") as f:
+            json.dump({"out": out}, f)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_ranks_word0_hash_collisions_bitwise(tmp_path):
+    import json
+
+    import torch.multiprocessing as mp
+    mp.spawn(_collide_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    runs = [json.load(open(os.path.join(tmp_path, f"collide{r}.json"))) for r in range(2)]
+    rows = _engine_rows()
+    _patch_hashes()
+    try:
+        from pipelinedp_amd import columnar
+        enc = columnar.encode_rows(rows, __import__("pipelinedp_amd").DataExtractors(
+            lambda r: r[0], lambda r: r[1], lambda r: r[2]))
+        assert enc.num_privacy_ids == len({r[0] for r in rows})  # 4 word-0 values, still every user distinct
+        want, _ = _run_engine(rows[0::2] + rows[1::2], None)
+    finally:
+        _unpatch_hashes()
+    assert len(want) > 5
+    for r in runs:
+        got = [(k, tuple(v)) for k, v in r["out"]]
+        assert [k for k, _ in got] == [k for k, _ in want]
+        for (_, g), (_, w) in zip(got, want):
+            np.testing.assert_array_equal(g, w)
+
+
 def test_aggregate_refuses_partials_k4_cannot_make(tmp_path):
     """A rank-local share of >= 2^32 rows with L_inf >= 131072 has no fixed-point
     partials (pdp_kernels.hip k4_enabled): World.aggregate raises before any

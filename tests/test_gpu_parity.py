@@ -38,12 +38,12 @@ BATCH_KERNEL = 4096  # debug flag: k_segments (register bitonic batches) instead
 NO_K4, K4_P16, K4_SOA, ODD_GRID = 1, 2, 4, 8  # debug flags (native.DEBUG_*): alternative forms
 
 
-def run_gpu(ex, pid, pk, val, U, P, bp: o.BoundParams, mask, seed=3, fallback=False, debug_flags=0):
+def run_gpu(ex, pid, pk, val, U, P, bp: o.BoundParams, mask, seed=3, fallback=False, debug_flags=0, debug_flags2=0):
     import torch
     from pipelinedp_amd.executor import BoundConfig
     cfg = BoundConfig(mask, bp.max_partitions_contributed, bp.max_contributions_per_partition, bp.min_value,
                       bp.max_value, bp.min_sum_per_partition, bp.max_sum_per_partition,
-                      bp.contribution_bounds_already_enforced, seed, fallback, debug_flags)
+                      bp.contribution_bounds_already_enforced, seed, fallback, debug_flags, debug_flags2)
     acc = ex.accumulate(_dev(pid, torch), _dev(pk, torch), _dev(val, torch), U, P, cfg)
     torch.cuda.synchronize()
     g = lambda t: None if t is None else t.cpu().numpy()  # noqa: E731
@@ -644,6 +644,43 @@ def test_k4_pair_record_forms_bitwise_equal(ex, cfgi):
                 assert b is None
             else:
                 np.testing.assert_array_equal(a, b)
+
+
+@pytest.mark.parametrize("mask", [1 | 2 | 4 | 16, 1 | 2])
+def test_hot_tables_dropped_on_whole_input_redo(ex, mask):
+    """Round-5 advisor finding: k_lean's K4 hot-partition tables flush their
+    kept groups (counts into the accumulators, sums into K4's fixed-point
+    scratch) before the host learns that the overflow list is full
+    (kCtrFull), which reruns EVERY row on the generic path.  Those groups must
+    be dropped then, or they count twice.  Debug flag OVERFLOW_FULL1 sets the
+    full flag from the second overflow range on (three privacy ids of 3000 rows
+    overflow here), while the hot tables hold Zipf-head pairs (L0 = 32).
+    Bit for bit against the oracle, with and without the flag."""
+    from pipelinedp_amd import native
+    n, U, P, z, L0, Linf, vb, _, _ = CONFIGS[11]
+    pid0, pk0, val0 = o.synth_rows(n, U, P, seed=811, zipf_s=z, value_lo=-5, value_hi=15)
+    rng = np.random.default_rng(811)
+    heavy = 3000
+    pid = np.concatenate([pid0] + [np.full(heavy, U + i, np.int64) for i in range(3)])
+    pk = np.concatenate([pk0] + [rng.integers(0, P, heavy) for _ in range(3)])
+    val = np.concatenate([val0, rng.uniform(-5, 15, 3 * heavy)])
+    perm = rng.permutation(len(pid))
+    pid, pk, val = pid[perm], pk[perm], val[perm]
+    bp = o.BoundParams(L0, Linf, *vb)
+    ref = o.bound_and_accumulate(pid, pk, val, P, bp, "hash", seed=19)
+    # the hot tables are in play here: they absorb pairs that would otherwise reach K4 as records
+    run_gpu(ex, pid, pk, val, U + 3, P, bp, mask, seed=19, debug_flags=native.DEBUG_NO_HOT_CACHE)
+    records_without_tables = ex.stats().k4_pairs
+    run_gpu(ex, pid, pk, val, U + 3, P, bp, mask, seed=19)
+    assert ex.stats().k4_pairs < records_without_tables
+    for flags2 in (0, native.DEBUG2_OVERFLOW_FULL1):
+        _, _, rc, cnt, x, y = run_gpu(ex, pid, pk, val, U + 3, P, bp, mask, seed=19, debug_flags2=flags2)
+        check_acc(ref, rc, cnt, x, y, mask, val, bp)
+        st = ex.stats()
+        if flags2:
+            assert st.fallback_rows == len(pid)  # the whole input went through the generic path
+        else:
+            assert 3 * heavy <= st.fallback_rows < len(pid)
 
 
 @pytest.mark.parametrize("p12", [True, False])

@@ -133,6 +133,68 @@ def test_hip_graph_capture_and_replay(ex):
     assert bool(same.all())
 
 
+def test_captured_release_survives_later_releases_with_larger_tables():
+    """A captured pdp_release points at the context's truncated-geometric
+    table.  Round 5 rewrote that table in place for another (eps, delta, L0),
+    or freed it for a larger one, so a graph captured earlier replayed the
+    wrong keep probabilities or a dangling pointer.  Tables are now immutable
+    per (eps, delta, L0) until the context is destroyed, and prepare_release
+    builds one outside the capture.  Capture accumulate + release; run eager
+    releases that need LARGER tables on the same executor; replay: bit for bit
+    the result of a fresh eager run.  An unprepared table under capture is
+    ERR_NEEDS_SYNC, not a host synchronisation inside the capture."""
+    import torch
+    from pipelinedp_amd import native
+    from pipelinedp_amd.executor import BoundConfig, HipExecutor, ReleaseConfig
+    ex3 = HipExecutor(0)
+    pid, pk, val, U, P = _c3_like(seed=21)
+    cfg = BoundConfig(MASK, 4, 2, 0.0, 10.0, sampling_seed=5)
+    eps = [0.0, 0.0, 0.4, 0.0, 0.3, 0.3]
+    delta = [0.0] * 5 + [1e-5]
+    rel = ReleaseConfig(MASK, native.NOISE_LAPLACE, native.SELECTION_TRUNCATED_GEOMETRIC, eps, delta, 1,
+                        add_noise=True, noise_seed=13)
+    # the later, eager releases: smaller selection eps / delta and larger L0 -> longer keep tables
+    others = [(0.05, 1e-8, 8), (0.02, 1e-9, 16)]
+    n0 = len(native.truncated_geometric_table(0.3, 1e-5, 4))
+    assert all(len(native.truncated_geometric_table(e, d, k)) > n0 for e, d, k in others)
+    d_pid, d_pk, d_val = _dev(pid), _dev(pk), _dev(val)
+
+    ex3.prepare_release(rel, cfg)  # the table, built outside the capture
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        ex3.accumulate(d_pid, d_pk, d_val, U, P, cfg, sync=False)  # warm-up: sizes the workspace
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    rel_new = ReleaseConfig(MASK, native.NOISE_LAPLACE, native.SELECTION_TRUNCATED_GEOMETRIC, eps,
+                            [0.0] * 5 + [3e-6], 1, add_noise=True, noise_seed=13)
+    with torch.cuda.graph(g):
+        acc = ex3.accumulate(d_pid, d_pk, d_val, U, P, cfg, sync=False)
+        keep, out, _ = ex3.release(acc, rel, cfg)
+        # an unprepared table inside the capture: refused, nothing enqueued, the capture stays valid
+        with pytest.raises(native.NativeError, match=r"\(-6\)"):
+            ex3.release(acc, rel_new, cfg)
+    for e, d, k in others:  # eager releases that need larger tables, on the same context
+        cfg_k = BoundConfig(MASK, k, 2, 0.0, 10.0, sampling_seed=5)
+        acc_k = ex3.accumulate(d_pid, d_pk, d_val, U, P, cfg_k)
+        ex3.release(acc_k, ReleaseConfig(MASK, native.NOISE_LAPLACE, native.SELECTION_TRUNCATED_GEOMETRIC,
+                                         [0.0, 0.0, 0.4, 0.0, 0.3, e], [0.0] * 5 + [d], 1, add_noise=True,
+                                         noise_seed=13), cfg_k)
+    torch.cuda.synchronize()
+    g.replay()
+    torch.cuda.synchronize()
+    assert ex3.status() == 0
+    # a fresh executor, eager
+    ex4 = HipExecutor(0)
+    acc4 = ex4.accumulate(d_pid, d_pk, d_val, U, P, cfg)
+    k4, o4, _ = ex4.release(acc4, rel, cfg)
+    torch.cuda.synchronize()
+    assert int(k4.sum()) > 0 and int(k4.sum()) < P
+    assert torch.equal(keep, k4)
+    assert bool(((out == o4) | (torch.isnan(out) & torch.isnan(o4))).all())
+
+
 def test_generic_path_input_redone_in_sync_mode_and_flagged_async(ex):
     """Privacy ids with > 2048 rows in a wave kernel need the host-driven
     generic path: a sync call redoes itself careful (more than one host wait,

@@ -158,17 +158,88 @@ def test_host_encoding():
     ex = pdp.DataExtractors(lambda r: r[0], lambda r: r[1], lambda r: r[2])
     e = encode_rows(rows, ex)
     assert e.partition_keys == ["a", "b", "c"] and e.pk.tolist() == [0, 1, 2, 0]
-    # privacy ids numbered by the ascending order of their key hash (columnar.dense_ids_from_hashes)
+    # privacy ids numbered by the ascending order of their 128-bit key hash (columnar.dense_ids_from_hashes)
     from pipelinedp_amd.columnar import key_hashes
     h = key_hashes(["u1", "u2", "u3"])
-    rank = {k: int(r) for k, r in zip(["u1", "u2", "u3"], np.argsort(np.argsort(h)))}
+    order = sorted(range(3), key=lambda i: (int(h[i, 0]), int(h[i, 1])))
+    rank = {["u1", "u2", "u3"][i]: r for r, i in enumerate(order)}
     assert e.pid.tolist() == [rank["u1"], rank["u2"], rank["u1"], rank["u3"]] and e.num_privacy_ids == 3
     # the hash is process-independent (blake2b of canonical bytes; numpy scalars / integral floats as ints)
-    assert key_hashes([5])[0] == key_hashes([np.int64(5)])[0] == key_hashes([5.0])[0]
-    assert len(set(key_hashes(["5", 5, (5,), b"5", None, 5.5]).tolist())) == 6
+    hk = lambda k: tuple(key_hashes([k])[0].tolist())  # noqa: E731
+    assert hk(5) == hk(np.int64(5)) == hk(5.0) == hk(5 + 0j)
+    assert hk(True) == hk(1) == hk(1.0) and hk(False) == hk(0) and hk((True, 2)) == hk((1, 2.0))
+    assert len({tuple(r) for r in key_hashes(["5", 5, (5,), b"5", None, 5.5]).tolist()}) == 6
     e = encode_rows(rows, ex, public_partitions=["c", "zz", "a", "c"])
     assert e.partition_keys == ["c", "zz", "a"] and e.pk.tolist() == [2, -1, 0, 2]
     np.testing.assert_array_equal(e.value, [1, 2, 3, 4])
+
+
+def _dict_groups(keys):
+    """The reference's privacy-id grouping: by dict key (pipeline_backend.py:476-485)."""
+    first = {}
+    return [first.setdefault(k, len(first)) for k in keys]
+
+
+def _same_partition(a, b):
+    """Two labelings of the same items induce the same grouping."""
+    a, b = list(a), list(b)
+    return all((a[i] == a[j]) == (b[i] == b[j]) for i in range(len(a)) for j in range(len(a)))
+
+
+MIXED_KEYS = [True, 1, 1.0, np.int64(1), "1", b"1", 2, 2.0, np.float32(2.0), False, 0, 0.0, -0.0, None, (1, 2),
+              (True, 2.0), (1, "2"), 3.5, np.float64(3.5), "u", "u", 1 + 0j, 7, "7"]
+
+
+def test_privacy_ids_grouped_by_dict_equality():
+    """True == 1 == 1.0 (and False == 0, numpy scalars, tuples of them) are ONE
+    dict key, so ONE privacy id in the reference; the encoding follows it
+    (round-5 advisor: bool and int canonicalised differently)."""
+    from pipelinedp_amd.columnar import encode_rows
+    rows = [(k, "p", 1.0) for k in MIXED_KEYS]
+    e = encode_rows(rows, pdp.DataExtractors(lambda r: r[0], lambda r: r[1], lambda r: r[2]))
+    assert _same_partition(e.pid, _dict_groups(MIXED_KEYS))
+    assert e.num_privacy_ids == len(set(_dict_groups(MIXED_KEYS)))
+    assert sorted(set(e.pid.tolist())) == list(range(e.num_privacy_ids))
+
+
+def test_privacy_ids_exact_under_forced_hash_collisions(monkeypatch):
+    """Every key hashed to the SAME 128-bit value (monkeypatched): distinct
+    keys must still be distinct privacy ids (told apart by their canonical
+    bytes, deterministic order), equal keys one id.  Then a non-binding
+    aggregate through DPEngine equals the reference's per-dict-key counts."""
+    from pipelinedp_amd import columnar
+    real = columnar.key_hashes
+    monkeypatch.setattr(columnar, "key_hashes", lambda keys: np.zeros((len(keys), 2), np.int64))
+    rows = [(k, "p", 1.0) for k in MIXED_KEYS]
+    ex = pdp.DataExtractors(lambda r: r[0], lambda r: r[1], lambda r: r[2])
+    e = columnar.encode_rows(rows, ex)
+    assert _same_partition(e.pid, _dict_groups(MIXED_KEYS))
+    # deterministic: the same ids in another input order
+    perm = list(reversed(range(len(rows))))
+    e2 = columnar.encode_rows([rows[i] for i in perm], ex)
+    assert [int(e2.pid[j]) for j in range(len(perm))] == [int(e.pid[i]) for i in perm]
+    # a partial collision (word 0 only) under the real hash: still exact, same grouping
+    monkeypatch.setattr(columnar, "key_hashes", lambda keys: real(keys) * np.array([[0, 1]], np.int64))
+    e3 = columnar.encode_rows(rows, ex)
+    assert _same_partition(e3.pid, _dict_groups(MIXED_KEYS))
+    # through the engine (tests/cpu_executor.py stands in for the GPU): non-binding bounds, so the
+    # privacy-id count of each partition is the number of distinct dict keys contributing to it
+    from cpu_executor import CpuExecutor
+    keys = MIXED_KEYS * 3
+    rows = [(k, f"part{i % 4}", 1.0) for i, k in enumerate(keys)]
+    backend = pdp.HipBackend(sampling_seed=5, noise_seed=9)
+    backend._executor = CpuExecutor()
+    acct = pdp.NaiveBudgetAccountant(total_epsilon=1e6, total_delta=1e-3)
+    engine = pdp.DPEngine(acct, backend)
+    params = pdp.AggregateParams(metrics=[pdp.Metrics.COUNT, pdp.Metrics.PRIVACY_ID_COUNT],
+                                 max_partitions_contributed=4, max_contributions_per_partition=100)
+    res = engine.aggregate(rows, params, ex, public_partitions=[f"part{j}" for j in range(4)])
+    acct.compute_budgets()
+    got = {k: v for k, v in res}
+    for j in range(4):
+        members = [r[0] for r in rows if r[1] == f"part{j}"]
+        assert round(got[f"part{j}"].privacy_id_count) == len(set(_dict_groups(members)))
+        assert round(got[f"part{j}"].count) == len(members)
 
 
 def test_hip_backend_host_ops_follow_local_backend():
