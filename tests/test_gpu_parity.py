@@ -374,7 +374,7 @@ def test_engine_matches_reference_golden(name, fallback):
     exp_keys = d["out_keys"].tolist()
     assert sorted(got) == sorted(exp_keys)
     fields = d["meta"]["fields"]
-    vmax = float(np.abs(d["value"]).max()) if has_val else 1.0
+    tol = _fp64_field_bounds(d, cfg, fields)
     for k, row in zip(exp_keys, d["out_vals"]):
         t = got[k]
         assert list(t._fields) == fields
@@ -383,8 +383,70 @@ def test_engine_matches_reference_golden(name, fallback):
             if f in ("count", "privacy_id_count"):
                 assert g == e, (k, f)
             else:
-                n = max(getattr(t, "count", 1.0), 1.0) if "count" in fields else 1000.0
-                assert abs(g - e) <= 1e-9 * (n + 1) * max(vmax, 1.0)**2 + 1e-9, (k, f, g, e)
+                assert abs(g - e) <= tol(k, f, dict(zip(fields, row))), (k, f, g, e, tol(k, f, dict(zip(fields, row))))
+
+
+U53 = 2.0**-53
+
+
+def _fp64_field_bounds(d, cfg, fields):
+    """Per-(partition, field) bound of |GPU - reference| for the noise-free
+    golden outputs: only the summation order differs (GPU: fixed-point pair
+    merge of input-order pair sums; reference: fp64 sums in its own order,
+    combiners.py:305-311,364-373), so for a sum of n terms
+        |s_gpu - s_ref| <= E = 4 (n + 2) 2^-53 sum|terms|
+    (both sides within (n + 2) u sum|t| of the exact sum, with a factor-2
+    margin), and means / variances carry it through compute_dp_mean / _var's
+    formulas (dp_computations.py:310-459) with a few ulps per operation.
+    n and sum|terms| are taken over ALL input rows of the partition (the kept
+    rows are a subset), so the bound holds whatever the bounding kept."""
+    m = set(cfg["metrics"])
+    keys = d["pk"]
+    v = d["value"] if len(d["value"]) else np.zeros(len(keys))
+    has_vb = "min_value" in cfg
+    a, b = (cfg.get("min_value", 0.0), cfg.get("max_value", 0.0))
+    mid = a + (b - a) / 2
+    meanlike = bool(m & {"mean", "variance"})
+    if meanlike:
+        t = np.clip(v, a, b) - mid
+    elif has_vb:
+        t = np.clip(v, a, b)
+    elif "min_sum_per_partition" in cfg:  # per-(pid, pk) sums clipped to [smin, smax]: |term| <= max(|smin|, |smax|)
+        t = np.full(len(keys), max(abs(cfg["min_sum_per_partition"]), abs(cfg["max_sum_per_partition"])))
+    else:
+        t = v
+    uk, inv = np.unique(keys, return_inverse=True)
+    n_rows = np.bincount(inv, minlength=len(uk)).astype(np.float64)
+    s1 = np.bincount(inv, weights=np.abs(t), minlength=len(uk))
+    s2 = np.bincount(inv, weights=t * t, minlength=len(uk))
+    where = {int(k): i for i, k in enumerate(uk)}
+
+    def bound(key, f, exp):
+        i = where.get(int(key))
+        n, S1, S2 = (n_rows[i], s1[i], s2[i]) if i is not None else (0.0, 0.0, 0.0)
+        ex = 4 * (n + 2) * U53 * S1
+        ey = 4 * (n + 2) * U53 * S2
+        c = max(float(exp.get("count", n)), 1.0)
+        tiny = 1e-300
+        if not meanlike:
+            return ex + tiny  # sum
+        mn = exp["mean"] - mid if "mean" in exp else 0.0
+        e_mn = ex / c + 2 * U53 * abs(mn)
+        e_mean = e_mn + 2 * U53 * (abs(mn) + abs(mid))
+        if f == "mean":
+            return e_mean + tiny
+        if f == "sum":
+            return c * e_mean + 2 * U53 * abs(exp.get("sum", 0.0)) + tiny
+        if f == "variance":
+            # dp_var = (nsumsq / c + mid of the squares interval) - mn^2 (compute_dp_var, compute_squares_interval)
+            sa, sb = (0.0, max(a * a, b * b)) if a < 0 < b else (a * a, b * b)
+            sq_mid = sa + (sb - sa) / 2 if sa != sb else 0.0
+            msq = exp["variance"] + mn * mn
+            e_msq = ey / c + 2 * U53 * (abs(msq) + 2 * abs(sq_mid))
+            return e_msq + 2 * abs(mn) * e_mn + e_mn * e_mn + 4 * U53 * (abs(msq) + mn * mn) + tiny
+        raise AssertionError(f)
+
+    return bound
 
 
 @pytest.mark.parametrize("fallback", [False, True])
