@@ -101,7 +101,14 @@ def parse():
     p.add_argument("--no-profile", action="store_true")
     p.add_argument("--seed", type=int, default=20250204)
     p.add_argument("--debug-flags", type=int, default=0, help="kernel ablation flags (experiments only)")
+    p.add_argument("--debug-flags2", type=int, default=0, help="second debug-flag word (A/B of alternative forms)")
     p.add_argument("--weak", action="store_true", help="c3: --rows / --pids per rank instead of node totals")
+    p.add_argument("--graph", action="store_true",
+                   help="capture one step (accumulate + release) in a hipGraph once and replay it in the timed "
+                        "loop (every kernel still runs every step); one GPU only")
+    p.add_argument("--share", type=int, default=0,
+                   help="one GPU runs the LAST rank's share of an N-GPU strong-scaling step (rows and privacy ids "
+                        "/ N, global ids via pid_base, no collective): the per-rank compute of SCALE, not SCALE")
     args = p.parse_args()
     for k, v in WORKLOADS[args.workload].items():
         if k != "strong" and getattr(args, k, None) is None:
@@ -113,9 +120,10 @@ def parse():
 def stage_bytes(stage, n_in, n_kept, P, nfields, survivors=0, survivor_passes=0, k4=None, y_slots=False):
     """Algorithmic bytes of one launch of each kernel (Roofline).
     With the L0 pre-filter (survivors > 0): K0 reads the privacy ids only, the
-    first pass is the bucket pass (+ a 4-B tag per row), k_filter reads the
-    tags three times (sketch, count, compaction) and moves the survivors'
-    records, and the survivor sort and K2 see the survivors only.  K4
+    first pass is the bucket pass (pid + pk in, 8-B {pk, row index} records +
+    4-B tags out), k_filter reads the tags twice (sketch, count) and gathers
+    the survivors (record, tag, value by row index), and the survivor sort and
+    K2 see the survivors only.  K4
     (k4 = (slots, pairs, passes)): K2 also writes one 16-B slot per sorted row,
     the first pair pass reads the slots and writes the pairs, later passes
     read + write the pairs, the reduction reads the pairs and writes
@@ -126,9 +134,13 @@ def stage_bytes(stage, n_in, n_kept, P, nfields, survivors=0, survivor_passes=0,
     slots, pairs, kpasses = k4 or (0, 0, 0)
     return {
         "histogram": (8 if survivors else 16) * n_in,  # read int64 pid (+ int64 pk)
-        "onesweep_first": (24 + 16 + (4 if survivors else 0)) * n_in,  # read 3 columns, write 16-B records (+ tags)
+        # pre-filter bucket pass (round 6): read pid + pk, write 8-B {pk, row index} records + 4-B tags;
+        # otherwise read 3 columns, write 16-B records
+        "onesweep_first": (16 + 8 + 4 if survivors else 24 + 16) * n_in,
         "onesweep_rest": 32 * n_kept,  # read + write 16-B records
-        "filter": 12 * n_kept + 32 * survivors,  # tags three times, survivors' records read + written
+        # tags twice (sketch, count) + keep bytes written and read; per survivor its 8-B record, its tag, its value
+        # (gathered from the input column by row index) read and its 16-B record written
+        "filter": 8.5 * n_kept + (8 + 4 + 8 + 16) * survivors,
         # histogram read + per pass (read + write) + per later pass an upsweep read
         "survivor_sort": survivors * (16 + 32 * survivor_passes + 16 * max(survivor_passes - 1, 0)),
         "buckets": 16 * sorted_rows + (32 if y_slots else 16) * slots,  # read 16-B records once (+ K4: write the pair slots)
@@ -350,11 +362,14 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         world = World(rank, world_size)
 
-    n = int(args.rows // world_size) if args.strong else int(args.rows)
+    # --share N: this single GPU plays rank N-1 of an N-GPU strong-scaling run (ids rebased, hashed globally)
+    split = args.share if args.share > 1 and world_size == 1 else world_size
+    vrank = split - 1 if args.share > 1 and world_size == 1 else rank
+    n = int(args.rows // split) if args.strong else int(args.rows)
     P = int(args.partitions)
-    U = int(args.pids // world_size) if args.strong else int(args.pids)
+    U = int(args.pids // split) if args.strong else int(args.pids)
     ex = HipExecutor(local)
-    pid, pk, val = ex.generate(n, U, P, seed=args.seed, zipf_s=args.zipf, lo=0.0, hi=10.0, row_offset=rank * n)
+    pid, pk, val = ex.generate(n, U, P, seed=args.seed, zipf_s=args.zipf, lo=0.0, hi=10.0, row_offset=vrank * n)
     # Multi-GPU: rank r's rows carry its own privacy ids (global id = r * U + local id), so every privacy id
     # lives on one rank (pid-sharded input); the sort uses the dense local ids.
     public = WORKLOADS[args.workload]["public"]
@@ -373,7 +388,8 @@ def main():
     # rank r's privacy ids are global ids r * U + local id: the sampling hashes the global id (pid_base, ABI 3),
     # so an N-GPU step bounds exactly what one process over the concatenated rows would
     bounds = BoundConfig(mask, args.l0, args.linf, 0.0, 10.0, sampling_seed=args.seed + 1,
-                         debug_flags=args.debug_flags, pid_base=rank * U if world_size > 1 else 0)
+                         debug_flags=args.debug_flags, debug_flags2=args.debug_flags2,
+                         pid_base=vrank * U if split > 1 else 0)
     # NaiveBudgetAccountant(eps=1, delta=1e-6): MeanCombiner (Laplace) eps 0.5, selection eps 0.5 delta 1e-6
     eps = [0.0] * 6
     delta = [0.0] * 6
@@ -414,11 +430,35 @@ def main():
     torch.cuda.synchronize()
     check_status()
     st = ex.stats()
+    run = step
+    graph_res = None
+    if args.graph:
+        # one step captured once (tests/test_gpu_stream_order.py: replay == eager bit for bit); the release's
+        # selection table is built before the capture (pdp_prepare_release)
+        if world is not None or sweep:
+            raise SystemExit("--graph: one GPU, aggregate workloads only")
+        ex.prepare_release(rel, bounds)
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            step()
+        torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize()
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            graph_res = step()
+        graph.replay()
+        torch.cuda.synchronize()
+        check_status()
+
+        def run():
+            graph.replay()
+            return graph_res
     rows_after_public_filter = int(st.kept_rows_in)
     surv = int(st.filter_rows)  # rows that survive the L0 pre-filter (0: it did not run)
     surv_passes = int(st.sort_passes) - 1 if surv else 0
     k4 = (int(st.k4_slots), int(st.k4_pairs), int(st.k4_passes)) if st.k4_slots else None
-    if not args.no_profile:
+    if not args.no_profile and not args.graph:
         ex.profile(True)
         ex.profile_read(reset=True)
     if world is not None:
@@ -428,7 +468,7 @@ def main():
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
     ev[0].record()
     for i in range(args.steps):
-        res = step()
+        res = run()
         ev[i + 1].record()  # per-step stamps for the median (no host wait inside the timed loop)
     torch.cuda.synchronize()
     if world is not None:
@@ -443,6 +483,15 @@ def main():
 
     roofline = None
     stages = {}
+    if not args.no_profile and args.graph:
+        # replays record no per-stage events: the stage times come from as many eager profiled steps, run after
+        # the graph-timed loop
+        ex.profile(True)
+        ex.profile_read(reset=True)
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize()
+        check_status()
     if not args.no_profile:
         prof = ex.profile_read(reset=True)
         ex.profile(False)
@@ -471,7 +520,9 @@ def main():
                     **({"bound_note": "c5 kernels are fp64-VALU bound (per-(pair, configuration) SumMetrics terms, "
                                       "Poisson-binomial pmf per partition); the HBM fraction is reported for "
                                       "completeness only"} if sweep else {}),
-                    "ms_per_launch_source": "hipEvents on the launch stream, averaged over the timed steps"}
+                    "ms_per_launch_source": "hipEvents on the launch stream, averaged over the timed steps" +
+                                            (" (--graph: over as many eager profiled steps after the graph-timed "
+                                             "loop)" if args.graph else "")}
         if sweep:
             # fp64-VALU bound: FLOP/s of k_ana_metrics against the box's measured fp64 FMA rate
             import ctypes
@@ -504,7 +555,7 @@ def main():
                 "pairs_kept_after_bounding": int(acc.row_count.sum().item())}
         del acc
 
-    rows_per_s = n * world_size * args.steps / elapsed
+    rows_per_s = n * world_size * args.steps / elapsed  # (--share: one rank's rows, this GPU alone)
     step_s = sorted(ev[i].elapsed_time(ev[i + 1]) * 1e-3 for i in range(args.steps))
     med = step_s[len(step_s) // 2] if len(step_s) % 2 else 0.5 * (step_s[len(step_s) // 2 - 1] + step_s[len(step_s) // 2])
     copy_gbs = copy_peak_gbs(torch, native.lib()) if rank == 0 and not args.no_profile else None
@@ -535,6 +586,11 @@ def main():
                            "total wall time between the synchronised brackets",
             "host_waits_per_step": int(ex.stats().host_waits) if not sweep else None,
             "scaling": "strong" if args.strong else "weak", "vs_baseline": None, "dtype": "f64",
+            "launch": "hipGraph replay of one captured step" if args.graph else "eager stream-ordered launches",
+            **({"rank_share": {"of_gpus": split, "rank": vrank, "pid_base": vrank * U,
+                               "label": "ONE GPU running one rank's share of an N-GPU strong-scaling c3 step "
+                                        "(rows and privacy ids / N, all partitions; no collective) -- not SCALE"}}
+               if split > 1 and world_size == 1 else {}),
             "data": "synthetic (on-device Philox generator, oracle/pdp_oracle.py:synth_rows)",
             "config": {"workload": (f"c5: UtilityAnalysisEngine.analyze, {len(SWEEP)} configurations "
                                     f"(L0 1..128 x Linf 1..8, sum bounds {SWEEP_SUM_BOUNDS}), COUNT+SUM+PRIVACY_ID_COUNT "

@@ -268,6 +268,7 @@ constexpr int kDebugDevOcc2 = 512;          // device-sized look-back passes at 
 constexpr int kDebugK4Compact = 1024;       // K2 writes compacted K4 pair records (k4_claim) instead of a slot per row
 // Second word of testing flags (pdp_bound_params.reserved2; the first word's 31 bits are taken).
 constexpr int kDebug2OverflowFull1 = 1;     // a second overflow range already sets kCtrFull (the whole-input redo)
+constexpr int kDebug2FilterRec16 = 2;       // the pre-filter's bucket pass carries 16-byte records (round-5 form)
 // Timing ablations whose results are invalid: accepted only by a -DPDP_DEBUG_BUILD library.
 constexpr int kAblationFlags = kDebugSortOnly | kDebugNoLookback | kDebugLinearWrite | kDebugNoScatter |
                                kDebugNoAtomics | kDebugWalkOnly | kDebugNoLinf | kDebugNoSums | kDebugFilterTiming;
@@ -781,7 +782,11 @@ __device__ __forceinline__ uint32_t xcd_tile(uint32_t b, uint32_t nwg) {
 // Returns false when the claimed tile lies beyond the row count (the block is done): the look-back
 // wrappers loop over tiles claimed in order, so a grid smaller than the tile count (sized from a host
 // upper bound while the row count lives in device memory) covers every tile.
-template <bool SOA, bool TAG = false, int P12 = 0, bool ANA = false>
+// TAG 2 (round 6): the bucket pass does not carry the values at all -- a row's record is 8 bytes
+// {pk, row index} (rows < 2^32: the pre-filter needs the reduce-then-scan passes), and k_filter gathers
+// the value of each SURVIVOR from the input column by its row index.  The pass reads 16 instead of 24 B
+// and writes 12 instead of 20 B per row.  TAG 1: the round-5 16-byte records {tag, pk, value}.
+template <bool SOA, int TAG = 0, int P12 = 0, bool ANA = false>
 __device__ __forceinline__ bool onesweep_body(
     const int64_t* __restrict__ pid, const int64_t* __restrict__ pk, const double* __restrict__ val,
     const Rec* __restrict__ rin, Rec* __restrict__ rout, int64_t n_in,
@@ -845,7 +850,10 @@ __device__ __forceinline__ bool onesweep_body(
       a[k] = ld_soa(pid + ic);
       b[k] = ld_soa(pk + ic);
     }
-    if (val) {
+    if constexpr (TAG == 2) {  // the row index rides in the value slot (k_filter gathers the value)
+#pragma unroll
+      for (int k = g; k < g + kSoaGroup && k < kItems; ++k) r[k].val = __longlong_as_double(base + k * 64);
+    } else if (val) {
 #pragma unroll
       for (int k = g; k < g + kSoaGroup && k < kItems; ++k) {
         const int64_t idx = base + k * 64;
@@ -1111,6 +1119,8 @@ __device__ __forceinline__ bool onesweep_body(
         }
 #endif
         if constexpr (P12 != 0) k4_st12(rout, q, rc);
+        else if constexpr (TAG == 2)
+          reinterpret_cast<uint2*>(rout)[q] = make_uint2(rc.pk, (uint32_t)__double_as_longlong(rc.val));
         else st_rec(rout + q, rc);
         if constexpr (TAG) tag_out[q] = rc.pid;
       }
@@ -1153,39 +1163,44 @@ __device__ __forceinline__ bool onesweep_body(
     __syncthreads();
 // records -> records (passes >= 1 of the pid sort, generic path, utility analysis)
 __global__ __launch_bounds__(kThreads, PDP_OS_OCC) void k_onesweep(PDP_ONESWEEP_ARGS) {
-  onesweep_body<false, false>(PDP_ONESWEEP_PASS);
+  onesweep_body<false, 0>(PDP_ONESWEEP_PASS);
 }
 // ... over a device-side record count (the L0 pre-filter's survivors)
 template <int OCC>
 __global__ __launch_bounds__(kThreads, OCC) void k_onesweep_dev(PDP_ONESWEEP_ARGS) {
-  PDP_ONESWEEP_LOOP(onesweep_body, false, false, 0, false)
+  PDP_ONESWEEP_LOOP(onesweep_body, false, 0, 0, false)
 }
 // SoA columns -> records (first pass of the pid sort, non-public rows dropped)
 __global__ __launch_bounds__(kThreads, PDP_OS_OCC) void k_sort_first(PDP_ONESWEEP_ARGS) {
-  onesweep_body<true, false>(PDP_ONESWEEP_PASS);
+  onesweep_body<true, 0>(PDP_ONESWEEP_PASS);
 }
 // the utility analysis' first (pk, pid) pass from the SoA columns (pdp_analysis.inc)
 __global__ __launch_bounds__(kThreads, PDP_OS_OCC) void k_ana_sort_first(PDP_ONESWEEP_ARGS) {
-  onesweep_body<true, false, 0, true>(PDP_ONESWEEP_PASS);
+  onesweep_body<true, 0, 0, true>(PDP_ONESWEEP_PASS);
 }
-// the L0 pre-filter's bucket pass (SoA columns -> tagged records + tags, pdp_filter.inc)
+// the L0 pre-filter's bucket pass (SoA pid / pk columns -> 8-byte {pk, row index} records + tags,
+// pdp_filter.inc)
 __global__ __launch_bounds__(kThreads, PDP_OS_OCC) void k_bucket_pass(PDP_ONESWEEP_ARGS) {
-  onesweep_body<true, true>(PDP_ONESWEEP_PASS);
+  onesweep_body<true, 2>(PDP_ONESWEEP_PASS);
+}
+// ... round-5 form (debug2 flag FILTER_REC16): 16-byte {tag, pk, value} records
+__global__ __launch_bounds__(kThreads, PDP_OS_OCC) void k_bucket_pass16(PDP_ONESWEEP_ARGS) {
+  onesweep_body<true, 1>(PDP_ONESWEEP_PASS);
 }
 // K4 pair records by partition block (pdp_reduce.inc); device-side record counts
 template <int OCC>
 __global__ __launch_bounds__(kThreads, OCC) void k_pair_pass(PDP_ONESWEEP_ARGS) {
-  PDP_ONESWEEP_LOOP(onesweep_body, false, false, 0, false)
+  PDP_ONESWEEP_LOOP(onesweep_body, false, 0, 0, false)
 }
 // ... with 12-byte pair records (K2 writes its slots in that form)
 template <int OCC>
 __global__ __launch_bounds__(kThreads, OCC) void k_pair_pass12(PDP_ONESWEEP_ARGS) {
-  PDP_ONESWEEP_LOOP(onesweep_body, false, false, 2, false)
+  PDP_ONESWEEP_LOOP(onesweep_body, false, 0, 2, false)
 }
 // ... whose first pass reads K2's split slots (keys, then the values of the non-empty ones)
 template <int OCC>
 __global__ __launch_bounds__(kThreads, OCC) void k_pair_pass12s(PDP_ONESWEEP_ARGS) {
-  PDP_ONESWEEP_LOOP(onesweep_body, false, false, 3, false)
+  PDP_ONESWEEP_LOOP(onesweep_body, false, 0, 3, false)
 }
 
 // Clears the look-back status words of the tiles of *rows_dev + add rows (a row count that lives in
@@ -3105,6 +3120,7 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
   const FilterPlan fpl = filter_plan(n, U, bp, sp.debug, sweep, rts);
   uint32_t* tags = (uint32_t*)(ws + L.tags);
   uint32_t* tag_lo = (uint32_t*)(ws + L.tag_lo);
+  const bool rec16 = (bp->reserved2 & kDebug2FilterRec16) != 0;  // round-5 bucket records (A/B, parity)
   ctx->last_filter = fpl.on;
   if (fpl.on) {
     ks.mode = 4;
@@ -3149,7 +3165,7 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
     }
     ProfScope ps(ctx, p == 0 ? PDP_STAGE_ONESWEEP_FIRST : PDP_STAGE_ONESWEEP_REST, stream);
     if (p == 0 && fpl.on)
-      hipLaunchKernelGGL(k_bucket_pass, dim3((unsigned)L.tiles), dim3(kThreads), 0, stream, cols->pid,
+      hipLaunchKernelGGL(rec16 ? k_bucket_pass16 : k_bucket_pass, dim3((unsigned)L.tiles), dim3(kThreads), 0, stream, cols->pid,
                          cols->pk, cols->value, (const Rec*)nullptr, dst, n, counters, (int)kCtrNKept, ks, p,
                          off + p * kHist, status, ctx->epoch, counters, (int)ctx->tile_slot++, bases, tags, tag_lo,
                          (const Rec*)nullptr, (int64_t)INT64_MAX);
@@ -3181,8 +3197,9 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
     HIP_TRY(zero_async(counters + kCtrNSurv, 8, stream));
     {
       ProfScope ps(ctx, PDP_STAGE_FILTER, stream);
-      hipLaunchKernelGGL(fpl.half ? k_filter<true> : k_filter<false>, dim3(256), dim3(kFiltThreads), 0, stream,
-                         sorted, tags, tag_lo, spare,
+      hipLaunchKernelGGL(fpl.half ? (rec16 ? k_filter<true, false> : k_filter<true, true>)
+                                  : (rec16 ? k_filter<false, false> : k_filter<false, true>),
+                         dim3(256), dim3(kFiltThreads), 0, stream, sorted, cols->value, tags, tag_lo, spare,
                          (uint8_t*)(ws + L.keep), off, counters,
                          (int)kCtrNKept, (int)kCtrNSurv, (int)bp->max_partitions_contributed,
                          (sp.debug & kDebugFilterTiming) != 0);

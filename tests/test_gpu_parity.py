@@ -105,9 +105,11 @@ FILTER_MAX_L0 = 8
 
 
 @pytest.mark.parametrize("mode", ["lean", "lean_min_search", "batch", "fallback", "filter", "filter_lean",
-                                  "filter_batch", "filter_fallback"])
+                                  "filter_batch", "filter_fallback", "filter_rec16"])
 @pytest.mark.parametrize("cfgi", range(len(CONFIGS)))
 def test_bound_accumulate_matches_oracle(ex, cfgi, mode):
+    """filter*: the L0 pre-filter forced on.  Its bucket pass carries 8-byte {pk, row index} records and
+    k_filter gathers the survivors' values (round 6); filter_rec16: the round-5 16-byte records."""
     n, U, P, z, L0, Linf, vb, pb, mask = CONFIGS[cfgi]
     pid, pk, val = o.synth_rows(n, U, P, seed=100 + cfgi, zipf_s=z, value_lo=-5, value_hi=15)
     bp = o.BoundParams(L0, Linf, *(vb or (None, None)), *(pb or (None, None)))
@@ -116,8 +118,9 @@ def test_bound_accumulate_matches_oracle(ex, cfgi, mode):
                                   fallback=mode in ("fallback", "filter_fallback"),
                                   debug_flags={"batch": BATCH_KERNEL, "lean_min_search": LEAN_MIN_SEARCH,
                                                "filter": FORCE_FILTER, "filter_fallback": FORCE_FILTER,
-                                               "filter_lean": FORCE_FILTER | NO_THIN,
-                                               "filter_batch": FORCE_FILTER | BATCH_KERNEL}.get(mode, 0))
+                                               "filter_lean": FORCE_FILTER | NO_THIN, "filter_rec16": FORCE_FILTER,
+                                               "filter_batch": FORCE_FILTER | BATCH_KERNEL}.get(mode, 0),
+                                  debug_flags2=2 if mode == "filter_rec16" else 0)
     ref = o.bound_and_accumulate(pid, pk, val if need_val else None, P, bp, "hash", seed=77 + cfgi)
     check_acc(ref, rc, cnt, x, y, mask, val, bp)
     st = ex.stats()
@@ -153,6 +156,11 @@ def test_prefilter_matches_unfiltered_at_scale(ex, L0, Linf, z, rows_per_pid):
     np.testing.assert_allclose(x, x2, rtol=1e-9, atol=1e-9)
     ref = o.bound_and_accumulate(pid, pk, val, P, bp, "hash", seed=9)
     check_acc(ref, rc, cnt, x, None, mask, val, bp)
+    # the round-5 bucket records (16 bytes, values carried) give the same survivors and accumulators, bit for bit
+    _, _, rc3, cnt3, x3, _ = run_gpu(ex, pid, pk, val, U, P, bp, mask, seed=9, debug_flags2=2)
+    assert ex.stats().filter_rows == surv
+    for a, b in ((rc, rc3), (cnt, cnt3), (x, x3)):
+        np.testing.assert_array_equal(a, b)
 
 
 def test_full_width_privacy_ids_and_wide_partition_ids(ex):

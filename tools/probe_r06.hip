@@ -83,6 +83,79 @@ __global__ void k_stream_read(const uint4* p, int64_t n16, unsigned int* out) {
   if (acc == 0x12345678u) out[threadIdx.x] = acc;
 }
 
+// (3) sparse gathers: the L0 pre-filter's survivors (6.8 % of 1e9 rows) gathered from the ORIGINAL pk / value
+// columns by row index instead of being carried through the bucket pass.  256 workgroups (one per privacy-id
+// bucket), each with a sorted list of ~265K row indices spread over the whole column (survivors keep input
+// order within a bucket): read the list (4 B), gather pk (8 B) and value (8 B), write a 16-B record.
+__global__ void k_make_lists(uint32_t* list, int64_t per, int64_t stride) {
+  const int64_t b = blockIdx.y;
+  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < per; k += (int64_t)gridDim.x * blockDim.x)
+    list[b * per + k] = (uint32_t)(k * stride + (int64_t)(mix64(((uint64_t)b << 40) ^ (uint64_t)k) % (uint64_t)stride));
+}
+
+template <int G>
+__global__ __launch_bounds__(1024) void k_sparse_gather(const uint32_t* list, int64_t per, const int64_t* pk,
+                                                         const double* val, uint4* out) {
+  const int64_t b = blockIdx.x;
+  const uint32_t* l = list + b * per;
+  for (int64_t k0 = threadIdx.x; k0 < per; k0 += 1024 * G) {
+    uint32_t idx[G];
+    int64_t p[G];
+    double v[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) idx[g] = k0 + g * 1024 < per ? l[k0 + g * 1024] : 0u;
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      p[g] = pk[idx[g]];
+      v[g] = val[idx[g]];
+    }
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      if (k0 + g * 1024 < per) {
+        const uint64_t vb = (uint64_t)__double_as_longlong(v[g]);
+        out[b * per + k0 + g * 1024] = uint4{idx[g], (uint32_t)p[g], (uint32_t)vb, (uint32_t)(vb >> 32)};
+      }
+    }
+  }
+}
+
+static void sparse_probe() {
+  const int64_t N = 1000000000ll, per = 265000, stride = N / per;
+  int64_t* pk = nullptr;
+  double* val = nullptr;
+  uint32_t* list = nullptr;
+  uint4* out = nullptr;
+  CK(hipMalloc(&pk, N * 8));
+  CK(hipMalloc(&val, N * 8));
+  CK(hipMalloc(&list, 256 * per * 4));
+  CK(hipMalloc(&out, 256 * per * 16));
+  CK(hipMemset(pk, 1, N * 8));
+  CK(hipMemset(val, 2, N * 8));
+  hipLaunchKernelGGL(k_make_lists, dim3(64, 256), dim3(256), 0, 0, list, per, stride);
+  CK(hipDeviceSynchronize());
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a));
+  CK(hipEventCreate(&b));
+  for (int rep = 0; rep < 2; ++rep) {
+    for (int G : {1, 4, 8}) {
+      CK(hipEventRecord(a, 0));
+      if (G == 1) hipLaunchKernelGGL(k_sparse_gather<1>, dim3(256), dim3(1024), 0, 0, list, per, pk, val, out);
+      if (G == 4) hipLaunchKernelGGL(k_sparse_gather<4>, dim3(256), dim3(1024), 0, 0, list, per, pk, val, out);
+      if (G == 8) hipLaunchKernelGGL(k_sparse_gather<8>, dim3(256), dim3(1024), 0, 0, list, per, pk, val, out);
+      CK(hipEventRecord(b, 0));
+      CK(hipEventSynchronize(b));
+      float ms = 0;
+      CK(hipEventElapsedTime(&ms, a, b));
+      std::printf("SPARSE_GATHER %lld survivors (256 x %lld, 1e9-row columns), %d in flight/lane: %.3f ms\n",
+                  (long long)(256 * per), (long long)per, G, ms);
+    }
+  }
+  CK(hipFree(pk));
+  CK(hipFree(val));
+  CK(hipFree(list));
+  CK(hipFree(out));
+}
+
 static int graph_probe() {
   hipStream_t s;
   CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
@@ -203,8 +276,10 @@ static void atomic_probe() {
 int main(int argc, char** argv) {
   const bool graph = argc < 2 || argv[1][0] == 'g' || argv[1][0] == 'a';
   const bool atom = argc < 2 || argv[1][0] == 't' || argv[1][0] == 'a';
+  const bool sparse = argc >= 2 && (argv[1][0] == 's' || argv[1][0] == 'a');
   int rc = 0;
   if (graph) rc = graph_probe();
   if (atom) atomic_probe();
+  if (sparse) sparse_probe();
   return rc;
 }
