@@ -117,13 +117,13 @@ def parse():
     return args
 
 
-def stage_bytes(stage, n_in, n_kept, P, nfields, survivors=0, survivor_passes=0, k4=None, y_slots=False):
+def stage_bytes(stage, n_in, n_kept, P, nfields, survivors=0, survivor_passes=0, k4=None, y_slots=False,
+                grouped=False):
     """Algorithmic bytes of one launch of each kernel (Roofline).
     With the L0 pre-filter (survivors > 0): K0 reads the privacy ids only, the
-    first pass is the bucket pass (pid + pk in, 8-B {pk, row index} records +
-    4-B tags out), k_filter reads the tags twice (sketch, count) and gathers
-    the survivors (record, tag, value by row index), and the survivor sort and
-    K2 see the survivors only.  K4
+    first pass is the bucket pass (+ a 4-B tag per row), k_filter reads the
+    tags twice (sketch, count) and moves the survivors' records, and the
+    survivor sort and K2 see the survivors only.  K4
     (k4 = (slots, pairs, passes)): K2 also writes one 16-B slot per sorted row,
     the first pair pass reads the slots and writes the pairs, later passes
     read + write the pairs, the reduction reads the pairs and writes
@@ -134,15 +134,15 @@ def stage_bytes(stage, n_in, n_kept, P, nfields, survivors=0, survivor_passes=0,
     slots, pairs, kpasses = k4 or (0, 0, 0)
     return {
         "histogram": (8 if survivors else 16) * n_in,  # read int64 pid (+ int64 pk)
-        # pre-filter bucket pass (round 6): read pid + pk, write 8-B {pk, row index} records + 4-B tags;
-        # otherwise read 3 columns, write 16-B records
-        "onesweep_first": (16 + 8 + 4 if survivors else 24 + 16) * n_in,
+        # read 3 columns, write 16-B records (+ the pre-filter's 4-B tags)
+        "onesweep_first": (24 + 16 + (4 if survivors else 0)) * n_in,
         "onesweep_rest": 32 * n_kept,  # read + write 16-B records
-        # tags twice (sketch, count) + keep bytes written and read; per survivor its 8-B record, its tag, its value
-        # (gathered from the input column by row index) read and its 16-B record written
-        "filter": 8.5 * n_kept + (8 + 4 + 8 + 16) * survivors,
-        # histogram read + per pass (read + write) + per later pass an upsweep read
-        "survivor_sort": survivors * (16 + 32 * survivor_passes + 16 * max(survivor_passes - 1, 0)),
+        # tags twice (sketch, count) + keep bytes written and read; per survivor its 16-B record read and written
+        "filter": 8.5 * n_kept + 32 * survivors,
+        # histogram read + per look-back pass (read + write); with the LDS grouping (survivor_group) the
+        # second pass's read + write moves to that stage
+        "survivor_sort": survivors * (16 + 32 * (survivor_passes - (1 if grouped else 0))),
+        "survivor_group": 32 * survivors,
         "buckets": 16 * sorted_rows + (32 if y_slots else 16) * slots,  # read 16-B records once (+ K4: write the pair slots)
         "pair_pass": 16 * slots + 16 * pairs + 32 * pairs * max(kpasses - 1, 0),
         "reduce": 16 * pairs + 24 * P,
@@ -505,7 +505,8 @@ def main():
                                   sel["ms_per_launch"] * sel["launches_per_step"]) / m["launches_per_step"]
         dom = max(stages, key=lambda s: stages[s]["ms_per_launch"] * stages[s]["launches_per_step"])
         nb = (P + world_size - 1) // world_size if world else P
-        b = stage_bytes(dom, n, rows_after_public_filter, nb, len(fields), surv, surv_passes, k4, variance)
+        b = stage_bytes(dom, n, rows_after_public_filter, nb, len(fields), surv, surv_passes, k4, variance,
+                        "survivor_group" in stages)
         ach = b / (stages[dom]["ms_per_launch"] * 1e-3) / 1e9
         traffic, prof_round = pmc_traffic(dom, n, args.workload) if not sweep else (None, None)
         roofline = {"bound": "hbm", "kernel": dom, "achieved": round(ach, 1), "peak": PEAK_HBM_GBS,
@@ -543,7 +544,8 @@ def main():
                         "ms_per_launch_source": "hipEvents on the launch stream (analysis_metrics minus the nested "
                                                 "analysis_select), averaged over the timed steps"}
         for s in stages:
-            bs = stage_bytes(s, n, rows_after_public_filter, nb, len(fields), surv, surv_passes, k4, variance)
+            bs = stage_bytes(s, n, rows_after_public_filter, nb, len(fields), surv, surv_passes, k4, variance,
+                             "survivor_group" in stages)
             if bs:
                 stages[s]["achieved_GBs"] = round(bs / (stages[s]["ms_per_launch"] * 1e-3) / 1e9, 1)
 

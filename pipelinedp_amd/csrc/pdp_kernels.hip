@@ -268,7 +268,11 @@ constexpr int kDebugDevOcc2 = 512;          // device-sized look-back passes at 
 constexpr int kDebugK4Compact = 1024;       // K2 writes compacted K4 pair records (k4_claim) instead of a slot per row
 // Second word of testing flags (pdp_bound_params.reserved2; the first word's 31 bits are taken).
 constexpr int kDebug2OverflowFull1 = 1;     // a second overflow range already sets kCtrFull (the whole-input redo)
-constexpr int kDebug2FilterRec16 = 2;       // the pre-filter's bucket pass carries 16-byte records (round-5 form)
+// the pre-filter's bucket pass carries 8-byte {pk, row index} records and k_filter gathers the survivors'
+// values by row index (round-6 experiment: bucket pass 9.13 -> 7.6 ms, filter 3.26 -> 5.2 ms: slower, r06c)
+constexpr int kDebug2FilterRec8 = 2;
+constexpr int kDebug2NoGroup = 4;        // survivor grouping by the round-5 second look-back pass, not k_group
+constexpr int kDebug2GroupFallback = 8;  // k_subruns hands every grouping to the look-back pass (kGrpBig = 1)
 // Timing ablations whose results are invalid: accepted only by a -DPDP_DEBUG_BUILD library.
 constexpr int kAblationFlags = kDebugSortOnly | kDebugNoLookback | kDebugLinearWrite | kDebugNoScatter |
                                kDebugNoAtomics | kDebugWalkOnly | kDebugNoLinf | kDebugNoSums | kDebugFilterTiming;
@@ -782,10 +786,12 @@ __device__ __forceinline__ uint32_t xcd_tile(uint32_t b, uint32_t nwg) {
 // Returns false when the claimed tile lies beyond the row count (the block is done): the look-back
 // wrappers loop over tiles claimed in order, so a grid smaller than the tile count (sized from a host
 // upper bound while the row count lives in device memory) covers every tile.
-// TAG 2 (round 6): the bucket pass does not carry the values at all -- a row's record is 8 bytes
-// {pk, row index} (rows < 2^32: the pre-filter needs the reduce-then-scan passes), and k_filter gathers
-// the value of each SURVIVOR from the input column by its row index.  The pass reads 16 instead of 24 B
-// and writes 12 instead of 20 B per row.  TAG 1: the round-5 16-byte records {tag, pk, value}.
+// TAG 1: the bucket pass's 16-byte records {tag, pk, value}.  TAG 2 (round-6 experiment, debug2 flag
+// FILTER_REC8): the pass does not carry the values -- a row's record is 8 bytes {pk, row index} (rows <
+// 2^32: the pre-filter needs the reduce-then-scan passes), and k_filter gathers the value of each SURVIVOR
+// from the input column by its row index.  The pass reads 16 instead of 24 B and writes 12 instead of 20
+// B per row (c3: 9.13 -> 7.6 ms), but the filter's two extra random gathers per survivor (value, tag)
+// cost more (3.26 -> 5.2 ms, r06c): off by default.
 template <bool SOA, int TAG = 0, int P12 = 0, bool ANA = false>
 __device__ __forceinline__ bool onesweep_body(
     const int64_t* __restrict__ pid, const int64_t* __restrict__ pk, const double* __restrict__ val,
@@ -1178,14 +1184,13 @@ __global__ __launch_bounds__(kThreads, PDP_OS_OCC) void k_sort_first(PDP_ONESWEE
 __global__ __launch_bounds__(kThreads, PDP_OS_OCC) void k_ana_sort_first(PDP_ONESWEEP_ARGS) {
   onesweep_body<true, 0, 0, true>(PDP_ONESWEEP_PASS);
 }
-// the L0 pre-filter's bucket pass (SoA pid / pk columns -> 8-byte {pk, row index} records + tags,
-// pdp_filter.inc)
+// the L0 pre-filter's bucket pass (SoA columns -> tagged 16-byte records + tags, pdp_filter.inc)
 __global__ __launch_bounds__(kThreads, PDP_OS_OCC) void k_bucket_pass(PDP_ONESWEEP_ARGS) {
-  onesweep_body<true, 2>(PDP_ONESWEEP_PASS);
-}
-// ... round-5 form (debug2 flag FILTER_REC16): 16-byte {tag, pk, value} records
-__global__ __launch_bounds__(kThreads, PDP_OS_OCC) void k_bucket_pass16(PDP_ONESWEEP_ARGS) {
   onesweep_body<true, 1>(PDP_ONESWEEP_PASS);
+}
+// ... debug2 flag FILTER_REC8: 8-byte {pk, row index} records (the values gathered by k_filter)
+__global__ __launch_bounds__(kThreads, PDP_OS_OCC) void k_bucket_pass8(PDP_ONESWEEP_ARGS) {
+  onesweep_body<true, 2>(PDP_ONESWEEP_PASS);
 }
 // K4 pair records by partition block (pdp_reduce.inc); device-side record counts
 template <int OCC>
@@ -1292,6 +1297,7 @@ __device__ __forceinline__ void emit_group(const SegParams& sp, const AccPtrs& a
   if (sp.want_y) atomicAdd(&acc.y[pk], y);
 }
 
+#include "pdp_group.inc"
 #include "pdp_reduce.inc"
 #include "pdp_segments.inc"
 #include "pdp_thin.inc"
@@ -1891,7 +1897,7 @@ hipError_t zero_async(void* p, size_t bytes, hipStream_t stream) {
 }
 
 struct Layout {
-  size_t recs_a, recs_b, recs_c, hist, off, counters, status, ranges, big, tags, tag_lo, keep, k4rep, k4s, total;
+  size_t recs_a, recs_b, recs_c, hist, off, counters, status, ranges, big, tags, tag_lo, keep, k4rep, k4s, grp, total;
   int64_t tiles;
   uint64_t big_cap;
 };
@@ -1918,6 +1924,8 @@ Layout layout_for(int64_t n, bool sweep = false, int64_t k4p = 0, bool variance 
   L.tags = o; o += sweep ? 0 : align_up((size_t)std::max<int64_t>(n, 1) * 4, 256);  // L0 pre-filter tags
   L.tag_lo = o; o += 256 * 4;
   L.keep = o; o += sweep ? 0 : align_up((size_t)std::max<int64_t>(n, 1) / 4 + 64, 256);  // k_filter keep bytes
+  // survivor grouping (pdp_group.inc): per-bucket low-byte histogram, claimed run bases, sub-run table, ctl
+  L.grp = o; o += sweep ? 0 : align_up(256 * 256 * 4 + 256 * 8 + (size_t)kGrpSubruns * 8 + 16, 256);
   L.k4rep = o; o += k4p > 0 ? align_up((size_t)kK4Rep * kK4MaxPasses * 256 * 4, 256) : 0;
   L.k4s = o; o += k4p > 0 ? align_up((size_t)k4p * 20, 256) : 0;
   L.total = o;
@@ -2178,7 +2186,9 @@ int sort_recs(pdp_ctx* ctx, Rec* a, Rec* b, int64_t m, const KeySpec& ks, unsign
               unsigned long long* off, unsigned long long* counters, unsigned long long* status, size_t status_bytes,
               void* ws, hipStream_t stream, Rec** out, int stage = PDP_STAGE_GENERIC,
               const int64_t* soa_pid = nullptr, const int64_t* soa_pk = nullptr, const double* soa_val = nullptr,
-              const unsigned long long* m_dev = nullptr) {
+              const unsigned long long* m_dev = nullptr, int run_passes = -1) {
+  // run_passes >= 0: histogram and offsets for all ks.passes, but only the first run_passes passes run
+  // (the survivor grouping finishes the last one in LDS, pdp_group.inc)
   // soa_pk != null: the utility analysis' rows, packed by the histogram and the first pass themselves
   // (k_histogram<2>, k_ana_sort_first); `a` is not read
   if (m <= 0 || ks.passes == 0) {
@@ -2207,7 +2217,8 @@ int sort_recs(pdp_ctx* ctx, Rec* a, Rec* b, int64_t m, const KeySpec& ks, unsign
   // sort 7.26 -> 6.48 ms (same box); PDP_SORT_TILESCAN=1 restores reduce-then-scan
   const bool rts = use_tile_scan(m, 0) && (ctx->cur_debug & kDebugSortTileScan) != 0 && !m_dev;
   const unsigned grid = m_dev ? (unsigned)std::min<int64_t>(tiles, kPersistGrid) : (unsigned)tiles;
-  for (int p = 0; p < ks.passes; ++p) {
+  const int npass = run_passes >= 0 ? std::min(run_passes, ks.passes) : ks.passes;
+  for (int p = 0; p < npass; ++p) {
     const unsigned int* bases = nullptr;
     // the fused first pass of the utility analysis reads the SoA columns: its tile counts would need
     // them too, so it always runs by look-back (k_tile_counts reads records)
@@ -3120,7 +3131,7 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
   const FilterPlan fpl = filter_plan(n, U, bp, sp.debug, sweep, rts);
   uint32_t* tags = (uint32_t*)(ws + L.tags);
   uint32_t* tag_lo = (uint32_t*)(ws + L.tag_lo);
-  const bool rec16 = (bp->reserved2 & kDebug2FilterRec16) != 0;  // round-5 bucket records (A/B, parity)
+  const bool rec16 = (bp->reserved2 & kDebug2FilterRec8) == 0;  // 16-byte bucket records (default)
   ctx->last_filter = fpl.on;
   if (fpl.on) {
     ks.mode = 4;
@@ -3165,7 +3176,7 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
     }
     ProfScope ps(ctx, p == 0 ? PDP_STAGE_ONESWEEP_FIRST : PDP_STAGE_ONESWEEP_REST, stream);
     if (p == 0 && fpl.on)
-      hipLaunchKernelGGL(rec16 ? k_bucket_pass16 : k_bucket_pass, dim3((unsigned)L.tiles), dim3(kThreads), 0, stream, cols->pid,
+      hipLaunchKernelGGL(rec16 ? k_bucket_pass : k_bucket_pass8, dim3((unsigned)L.tiles), dim3(kThreads), 0, stream, cols->pid,
                          cols->pk, cols->value, (const Rec*)nullptr, dst, n, counters, (int)kCtrNKept, ks, p,
                          off + p * kHist, status, ctx->epoch, counters, (int)ctx->tile_slot++, bases, tags, tag_lo,
                          (const Rec*)nullptr, (int64_t)INT64_MAX);
@@ -3195,6 +3206,11 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
   if (fpl.on) {
     // K1f: survivors of the bucket-sorted rows -> spare (input order per pid kept)
     HIP_TRY(zero_async(counters + kCtrNSurv, 8, stream));
+    unsigned int* shist = (unsigned int*)(ws + L.grp);
+    unsigned long long* sbase = (unsigned long long*)(shist + 256 * 256);
+    uint2* subruns = (uint2*)(sbase + 256);
+    unsigned long long* grp_ctl = (unsigned long long*)(subruns + kGrpSubruns);
+    HIP_TRY(zero_async(shist, 256 * 256 * 4 + 256 * 8, stream));  // buckets without rows claim nothing
     {
       ProfScope ps(ctx, PDP_STAGE_FILTER, stream);
       hipLaunchKernelGGL(fpl.half ? (rec16 ? k_filter<true, false> : k_filter<true, true>)
@@ -3202,7 +3218,7 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
                          dim3(256), dim3(kFiltThreads), 0, stream, sorted, cols->value, tags, tag_lo, spare,
                          (uint8_t*)(ws + L.keep), off, counters,
                          (int)kCtrNKept, (int)kCtrNSurv, (int)bp->max_partitions_contributed,
-                         (sp.debug & kDebugFilterTiming) != 0);
+                         (sp.debug & kDebugFilterTiming) != 0, shist, sbase);
     }
     HIP_TRY(hipGetLastError());
     // Survivors stably by pid & (2^low_bits - 1) only.  That groups every pid: within a bucket the
@@ -3222,9 +3238,35 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
     Rec* sa = spare;
     Rec* sb = sorted;
     Rec* out = nullptr;
+    // Two passes: the second one's work is done by k_group in LDS (pdp_group.inc) -- unless a sub-run is
+    // too long for it, which k_subruns decides on the device (the look-back pass then runs on every row).
+    const bool group = k2.passes == 2 && !(bp->reserved2 & kDebug2NoGroup);
     int rc = sort_recs(ctx, sa, sb, n, k2, hist, off, counters, status, status_bytes, workspace, stream, &out,
-                       PDP_STAGE_SURVIVOR_SORT, nullptr, nullptr, nullptr, counters + kCtrNSurv);
+                       PDP_STAGE_SURVIVOR_SORT, nullptr, nullptr, nullptr, counters + kCtrNSurv, group ? 1 : -1);
     if (rc) return rc;
+    if (group) {
+      ProfScope ps(ctx, PDP_STAGE_SURVIVOR_GROUP, stream);
+      Rec* dst = (out == sa) ? sb : sa;
+      hipLaunchKernelGGL(k_subruns, dim3(1), dim3(256), 0, stream, (const unsigned int*)shist,
+                         (const unsigned long long*)sbase, (const unsigned long long*)off,
+                         (const unsigned long long*)(counters + kCtrNSurv), subruns, grp_ctl,
+                         (bp->reserved2 & kDebug2GroupFallback) ? 1u : kGrpBig);
+      hipLaunchKernelGGL(k_group, dim3(2048), dim3(kGrpThreads), 0, stream, (const Rec*)out, dst,
+                         (const uint2*)subruns, (int)kGrpSubruns, k2.shift[1], k2.bits[1],
+                         (const unsigned long long*)grp_ctl);
+      // the look-back pass over grp_ctl[1] rows: 0 unless k_subruns fell back
+      next_epoch_dev(ctx, stream, status, grp_ctl + 1, 0, true);
+      const int occ = dev_occ(ctx->cur_debug);
+      auto dev_kern = occ == 2 ? k_onesweep_dev<2> : occ == 4 ? k_onesweep_dev<4> : k_onesweep_dev<3>;
+      const int64_t tiles = (n + kTile - 1) / kTile;
+      hipLaunchKernelGGL(dev_kern, dim3((unsigned)std::min<int64_t>(tiles, kPersistGrid)), dim3(kThreads), 0, stream,
+                         (const int64_t*)nullptr, (const int64_t*)nullptr, (const double*)nullptr, (const Rec*)out,
+                         dst, n, (const unsigned long long*)grp_ctl, 1, k2, 1, off + kHist, status, ctx->epoch,
+                         counters, (int)ctx->tile_slot++, (const unsigned int*)nullptr, (uint32_t*)nullptr,
+                         (const uint32_t*)nullptr, (const Rec*)nullptr, (int64_t)INT64_MAX);
+      HIP_TRY(hipGetLastError());
+      out = dst;
+    }
     sorted = out;
     spare = (out == sa) ? sb : sa;
     n_slot = kCtrNGeneric;

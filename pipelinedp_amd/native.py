@@ -37,7 +37,7 @@ DEBUG_K4_COMPACT = 1024  # K2 claims compacted K4 pair slots (one atomic counter
 DEBUG_THIN2 = 67108864  # K4 on: the LDS-staged k_thin2 instead of k_thin (measured slower)
 # second flag word (pdp_bound_params.reserved2)
 DEBUG2_OVERFLOW_FULL1 = 1  # a second overflow range already sets the "redo everything on the generic path" flag
-DEBUG2_FILTER_REC16 = 2  # the L0 pre-filter's bucket pass carries 16-byte {tag, pk, value} records (round-5 form)
+DEBUG2_FILTER_REC8 = 2  # L0 pre-filter bucket pass with 8-byte {pk, row index} records (measured slower, r06c)
 DEBUG_NO_HOT_CACHE = 524288  # K2 without its hot-partition table (K4 off: LDS atomics cache; K4 on: K4Hot)
 
 c_i32, c_i64, c_u64, c_f64 = ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64, ctypes.c_double
@@ -166,7 +166,7 @@ SIGNATURES = [
 
 STAGES = ["histogram", "onesweep_first", "onesweep_rest", "buckets", "generic", "release", "enforced",
           "tile_counts", "analysis_pairs", "analysis_metrics", "filter", "survivor_sort", "pair_pass", "reduce",
-          "analysis_sort", "analysis_aggregate", "analysis_select"]
+          "analysis_sort", "analysis_aggregate", "analysis_select", "survivor_group"]
 
 _lib = None
 

@@ -105,11 +105,11 @@ FILTER_MAX_L0 = 8
 
 
 @pytest.mark.parametrize("mode", ["lean", "lean_min_search", "batch", "fallback", "filter", "filter_lean",
-                                  "filter_batch", "filter_fallback", "filter_rec16"])
+                                  "filter_batch", "filter_fallback", "filter_rec8"])
 @pytest.mark.parametrize("cfgi", range(len(CONFIGS)))
 def test_bound_accumulate_matches_oracle(ex, cfgi, mode):
-    """filter*: the L0 pre-filter forced on.  Its bucket pass carries 8-byte {pk, row index} records and
-    k_filter gathers the survivors' values (round 6); filter_rec16: the round-5 16-byte records."""
+    """filter*: the L0 pre-filter forced on; filter_rec8: its bucket pass with 8-byte {pk, row index}
+    records, k_filter gathering the survivors' values (round-6 experiment, debug2 FILTER_REC8)."""
     n, U, P, z, L0, Linf, vb, pb, mask = CONFIGS[cfgi]
     pid, pk, val = o.synth_rows(n, U, P, seed=100 + cfgi, zipf_s=z, value_lo=-5, value_hi=15)
     bp = o.BoundParams(L0, Linf, *(vb or (None, None)), *(pb or (None, None)))
@@ -118,9 +118,9 @@ def test_bound_accumulate_matches_oracle(ex, cfgi, mode):
                                   fallback=mode in ("fallback", "filter_fallback"),
                                   debug_flags={"batch": BATCH_KERNEL, "lean_min_search": LEAN_MIN_SEARCH,
                                                "filter": FORCE_FILTER, "filter_fallback": FORCE_FILTER,
-                                               "filter_lean": FORCE_FILTER | NO_THIN, "filter_rec16": FORCE_FILTER,
+                                               "filter_lean": FORCE_FILTER | NO_THIN, "filter_rec8": FORCE_FILTER,
                                                "filter_batch": FORCE_FILTER | BATCH_KERNEL}.get(mode, 0),
-                                  debug_flags2=2 if mode == "filter_rec16" else 0)
+                                  debug_flags2=2 if mode == "filter_rec8" else 0)
     ref = o.bound_and_accumulate(pid, pk, val if need_val else None, P, bp, "hash", seed=77 + cfgi)
     check_acc(ref, rc, cnt, x, y, mask, val, bp)
     st = ex.stats()
@@ -156,11 +156,39 @@ def test_prefilter_matches_unfiltered_at_scale(ex, L0, Linf, z, rows_per_pid):
     np.testing.assert_allclose(x, x2, rtol=1e-9, atol=1e-9)
     ref = o.bound_and_accumulate(pid, pk, val, P, bp, "hash", seed=9)
     check_acc(ref, rc, cnt, x, None, mask, val, bp)
-    # the round-5 bucket records (16 bytes, values carried) give the same survivors and accumulators, bit for bit
+    # the 8-byte bucket records (values gathered by row index, debug2 FILTER_REC8): the same survivors and
+    # accumulators, bit for bit
     _, _, rc3, cnt3, x3, _ = run_gpu(ex, pid, pk, val, U, P, bp, mask, seed=9, debug_flags2=2)
     assert ex.stats().filter_rows == surv
     for a, b in ((rc, rc3), (cnt, cnt3), (x, x3)):
         np.testing.assert_array_equal(a, b)
+
+
+@pytest.mark.parametrize("L0,Linf,rows_per_pid,zipf", [(1, 1, 4, 0.0), (2, 3, 6, 1.1), (4, 2, 5, 1.3),
+                                                         (8, 4, 16, 0.0)])
+def test_survivor_grouping_forms_bitwise_equal(ex, L0, Linf, rows_per_pid, zipf):
+    """Privacy-id buckets wider than 256 ids (here U = 2^19: 2048 ids per bucket, 11 low bits) take two
+    survivor-grouping steps: the look-back pass on the low byte, then the LDS grouping of each (bucket,
+    low byte) sub-run (k_subruns + k_group, round 6).  Against the round-5 second look-back pass
+    (debug2 NO_GROUP) and the device-side fallback that hands every sub-run to that pass (debug2
+    GROUP_FALLBACK): identical accumulators, bit for bit, and the oracle's."""
+    n, P = 1 << 21, 50000
+    U = 1 << 19 if rows_per_pid < 16 else 1 << 17
+    pid, pk, val = o.synth_rows(n, U, P, seed=600 + L0, zipf_s=zipf, value_lo=-5, value_hi=15)
+    bp = o.BoundParams(L0, Linf, 0.0, 10.0)
+    mask = 1 | 2 | 4 | 16
+    runs = []
+    for flags2 in (0, 4, 8):  # default, NO_GROUP, GROUP_FALLBACK
+        _, _, rc, cnt, x, _ = run_gpu(ex, pid, pk, val, U, P, bp, mask, seed=13, debug_flags=FORCE_FILTER,
+                                      debug_flags2=flags2)
+        st = ex.stats()
+        assert st.filter_rows > 0 and st.sort_passes == 3  # bucket pass + two grouping steps
+        runs.append((rc, cnt, x))
+    for other in runs[1:]:
+        for a, b in zip(runs[0], other):
+            np.testing.assert_array_equal(a, b)
+    ref = o.bound_and_accumulate(pid, pk, val, P, bp, "hash", seed=13)
+    check_acc(ref, runs[0][0], runs[0][1], runs[0][2], None, mask, val, bp)
 
 
 def test_full_width_privacy_ids_and_wide_partition_ids(ex):
