@@ -171,6 +171,9 @@ struct KeySpec {
   uint64_t pid_base;  // the sampling hashes pid_base + pid (pdp_bound_params.pid_base)
   uint32_t num_parts;
   uint64_t mult;  // mode 4: bucket digit multiplier (pdp_filter.inc)
+  // the pre-filter's bucket pass (TAG): within a tile's run of a bucket, rows of sketch level <= tau come
+  // first (a stable split by one class bit; the order within a (pid, pk) group -- one level -- is kept)
+  int tau;
   int prof;  // accumulate per-phase s_memtime cycles of k_onesweep (kDebugSweepStamps)
   int ablate;  // kDebugNoLookback / kDebugLinearWrite (timing ablations, results invalid)
   int xcd_remap;  // reduce-then-scan passes: blocks sharing an XCD take one contiguous run of tiles
@@ -273,6 +276,7 @@ constexpr int kDebug2OverflowFull1 = 1;     // a second overflow range already s
 constexpr int kDebug2FilterRec8 = 2;
 constexpr int kDebug2NoGroup = 4;        // survivor grouping by the round-5 second look-back pass, not k_group
 constexpr int kDebug2GroupFallback = 8;  // k_subruns hands every grouping to the look-back pass (kGrpBig = 1)
+constexpr int kDebug2NoClassSplit = 16;  // bucket pass: no low-level-first order within a tile's bucket run
 // Timing ablations whose results are invalid: accepted only by a -DPDP_DEBUG_BUILD library.
 constexpr int kAblationFlags = kDebugSortOnly | kDebugNoLookback | kDebugLinearWrite | kDebugNoScatter |
                                kDebugNoAtomics | kDebugWalkOnly | kDebugNoLinf | kDebugNoSums | kDebugFilterTiming;
@@ -801,10 +805,16 @@ __device__ __forceinline__ bool onesweep_body(
     unsigned long long* __restrict__ counters, int tile_slot, const unsigned int* __restrict__ tile_base,
     uint32_t* __restrict__ tag_out, const uint32_t* __restrict__ tag_lo, const Rec* __restrict__ rin2,
     int64_t split) {
+  // TAG: the in-tile ranking key is the sub-digit 2 d + class (512 sub-digits, 512 dropped, 513 padding)
+  constexpr int kSub = TAG ? 2 : 1;
+  constexpr int kCntW = TAG ? 2 * 256 + 2 : kHist + 1;
+  constexpr int kDrShift = TAG ? 10 : 9;
+  constexpr uint32_t kDrMask = (1u << kDrShift) - 1u;
+  constexpr uint32_t kValidSub = 256u * kSub;  // sub-digits below this are placed rows
   __shared__ Rec s_rec[kHalfTile];
   __shared__ uint32_t s_lo[TAG ? 256 : 1];
-  __shared__ unsigned int s_cnt[4][kHist + 1];
-  __shared__ unsigned int s_dstart[256];
+  __shared__ unsigned int s_cnt[4][kCntW];
+  __shared__ unsigned int s_dstart[256 * kSub];
   __shared__ long long s_gbase[256];
   __shared__ unsigned int s_tmp[4];
   __shared__ unsigned int s_tile;
@@ -815,7 +825,7 @@ __device__ __forceinline__ bool onesweep_body(
   // Reduce-then-scan mode (tile_base != null): tile = block, its digit bases
   // are precomputed; otherwise tiles are claimed in order for the look-back.
   if (t == 0 && !tile_base) s_tile = (unsigned int)atomicAdd(&counters[tile_slot], 1ull);
-  for (int i = t; i < 4 * (kHist + 1); i += kThreads) (&s_cnt[0][0])[i] = 0;
+  for (int i = t; i < 4 * kCntW; i += kThreads) (&s_cnt[0][0])[i] = 0;
   if (TAG) s_lo[t] = tag_lo[t];
   __syncthreads();
   // Reduce-then-scan: any tile order is valid, so blocks that share an XCD
@@ -883,14 +893,17 @@ __device__ __forceinline__ bool onesweep_body(
         // placed unless the privacy id is out of range (k_histogram_tiles<true>); a non-public row
         // (pk < 0) is tagged dropped, an out-of-range pk is an error
         if (a[k] < 0 || a[k] >= (int64_t)ks.num_pids) {
-          d = 256;
+          d = 512;  // dropped (sub-digit space)
         } else {
           d = digit_of(ks, pass, r[k]);
           if (b[k] < 0 || b[k] >= (int64_t)ks.num_parts) {
             ninv += valid && b[k] >= 0;
             r[k].pid = kTagDropped | (d << 22);
+            d = 2u * d;
           } else {
-            r[k].pid = (d << 22) | ((r[k].pid - s_lo[d]) << 5) | filt_level(filt_prio(ks.seed, ks.pid_base + r[k].pid, r[k].pk));
+            const uint32_t lv = filt_level(filt_prio(ks.seed, ks.pid_base + r[k].pid, r[k].pk));
+            r[k].pid = (d << 22) | ((r[k].pid - s_lo[d]) << 5) | lv;
+            d = 2u * d + (lv > (uint32_t)ks.tau ? 1u : 0u);
           }
         }
       } else {
@@ -899,7 +912,7 @@ __device__ __forceinline__ bool onesweep_body(
         else
           d = digit_of(ks, pass, r[k]);
       }
-      dr[k] = valid ? d : 257u;  // 257: padding, ignored
+      dr[k] = valid ? d : (TAG ? 513u : 257u);  // 257 (TAG 513): padding, ignored
     }
    }
   } else {
@@ -956,6 +969,7 @@ __device__ __forceinline__ bool onesweep_body(
   const uint64_t lt = (1ull << lane) - 1ull;
   const bool any_invalid = SOA || ks.mode == 6 || tile_start + kTile > n_eff;
 #if PDP_OS_RANK_ATOMIC
+  static_assert(TAG == 0, "PDP_OS_RANK_ATOMIC variant builds do not rank the bucket pass's sub-digits");
   constexpr int kRankGroup = kItems < 8 ? kItems : 8;  // atomics in flight before their shuffles
 #pragma unroll
   for (int k0 = 0; k0 < kItems; k0 += kRankGroup) {
@@ -996,15 +1010,15 @@ __device__ __forceinline__ bool onesweep_body(
     const uint32_t d = dr[k];
     uint64_t peers = ~0ull;
 #pragma unroll
-    for (int b = 0; b < 8; ++b) {
-      if (b < radix_bits) {
+    for (int b = 0; b < (TAG ? 9 : 8); ++b) {
+      if (TAG || b < radix_bits) {
         const bool bit = (d >> b) & 1u;
         const uint64_t bb = __ballot(bit);
         peers &= bit ? bb : ~bb;
       }
     }
-    if (any_invalid) {  // digits 256 (dropped) / 257 (padding) share a counter
-      const bool v = d < 256;
+    if (any_invalid) {  // digits 256 (dropped) / 257 (padding) share a counter (TAG: 512 / 513)
+      const bool v = d < kValidSub;
       const uint64_t bb = __ballot(v);
       peers &= v ? bb : ~bb;
     }
@@ -1012,27 +1026,32 @@ __device__ __forceinline__ bool onesweep_body(
     const uint32_t c = __popcll(peers);
     const uint32_t basec = s_cnt[wave][d];
     __builtin_amdgcn_wave_barrier();
-    if (before == 0 && d < 256) s_cnt[wave][d] = basec + c;
+    if (before == 0 && d < kValidSub) s_cnt[wave][d] = basec + c;
     __builtin_amdgcn_wave_barrier();
-    dr[k] = d | ((basec + before) << 9);
+    dr[k] = d | ((basec + before) << kDrShift);
   }
   __syncthreads();
 #endif
 
   // Per-digit tile counts, per-wave exclusive offsets, digit starts.
-  unsigned int tcount = 0;
-  {
-    const unsigned int c0w = s_cnt[0][t], c1w = s_cnt[1][t], c2w = s_cnt[2][t], c3w = s_cnt[3][t];
-    tcount = c0w + c1w + c2w + c3w;
+  unsigned int tcount = 0, tcount0 = 0;
+#pragma unroll
+  for (int u = 0; u < kSub; ++u) {  // TAG: the digit's two sub-digits (class 0, then class 1)
+    const int sd = kSub * t + u;
+    const unsigned int c0w = s_cnt[0][sd], c1w = s_cnt[1][sd], c2w = s_cnt[2][sd], c3w = s_cnt[3][sd];
+    const unsigned int cs = c0w + c1w + c2w + c3w;
+    tcount += cs;
+    if (u == 0) tcount0 = cs;
     __syncthreads();
-    s_cnt[0][t] = 0;
-    s_cnt[1][t] = c0w;
-    s_cnt[2][t] = c0w + c1w;
-    s_cnt[3][t] = c0w + c1w + c2w;
+    s_cnt[0][sd] = 0;
+    s_cnt[1][sd] = c0w;
+    s_cnt[2][sd] = c0w + c1w;
+    s_cnt[3][sd] = c0w + c1w + c2w;
   }
   unsigned int total;
   const unsigned int dstart = block_excl_scan(tcount, s_tmp, total);
-  s_dstart[t] = dstart;
+  s_dstart[kSub * t] = dstart;
+  if (TAG) s_dstart[kSub * t + (kSub - 1)] = dstart + tcount0;
   if (t == 0) s_total = total;
 
   const long long c1 = ks.prof ? (long long)__builtin_amdgcn_s_memtime() : 0;
@@ -1093,8 +1112,8 @@ __device__ __forceinline__ bool onesweep_body(
   // Sorted position of every item in the tile.
 #pragma unroll
   for (int k = 0; k < kItems; ++k) {
-    const uint32_t d = dr[k] & 511u;
-    dr[k] = d < 256 ? s_dstart[d] + s_cnt[wave][d] + (dr[k] >> 9) : kNoPos;
+    const uint32_t d = dr[k] & kDrMask;
+    dr[k] = d < kValidSub ? s_dstart[d] + s_cnt[wave][d] + (dr[k] >> kDrShift) : kNoPos;
   }
   // Two halves: stage positions [h, h + kHalfTile) in LDS, write contiguous
   // digit runs (the digit is recomputed from the staged record).
@@ -3136,6 +3155,17 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
   if (fpl.on) {
     ks.mode = 4;
     ks.mult = fpl.mult;
+    // Rows likely to survive (sketch level <= tau) first within each tile's bucket run: the survivors then
+    // sit densely in the record array and k_filter's gather reads far fewer lines (c3: ~10 % of the rows
+    // are class 0 and hold most survivors).  tau ~ the level of the 3 L0 / (rows per pid) quantile of the
+    // priorities; a poor tau costs only speed (a (pid, pk) group has one level, so its rows keep their
+    // input order whatever tau is).
+    {
+      const double q = 3.0 * (double)bp->max_partitions_contributed * (double)U / (double)std::max<int64_t>(n, 1);
+      int tau = q >= 1.0 ? 31 : (int)std::floor(31.0 + 4.0 * std::log2(q));
+      tau = std::min(31, std::max(0, tau));
+      ks.tau = (bp->reserved2 & kDebug2NoClassSplit) ? 31 : tau;
+    }
     ks.passes = 1;
     ks.shift[0] = 64;
     ks.bits[0] = 8;
@@ -3247,11 +3277,12 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
     if (group) {
       ProfScope ps(ctx, PDP_STAGE_SURVIVOR_GROUP, stream);
       Rec* dst = (out == sa) ? sb : sa;
-      hipLaunchKernelGGL(k_subruns, dim3(1), dim3(256), 0, stream, (const unsigned int*)shist,
+      HIP_TRY(zero_async(grp_ctl, 16, stream));
+      hipLaunchKernelGGL(k_subruns, dim3(256), dim3(256), 0, stream, (const unsigned int*)shist,
                          (const unsigned long long*)sbase, (const unsigned long long*)off,
                          (const unsigned long long*)(counters + kCtrNSurv), subruns, grp_ctl,
                          (bp->reserved2 & kDebug2GroupFallback) ? 1u : kGrpBig);
-      hipLaunchKernelGGL(k_group, dim3(2048), dim3(kGrpThreads), 0, stream, (const Rec*)out, dst,
+      hipLaunchKernelGGL(k_group, dim3(4096), dim3(64 * kGrpBlockWaves), 0, stream, (const Rec*)out, dst,
                          (const uint2*)subruns, (int)kGrpSubruns, k2.shift[1], k2.bits[1],
                          (const unsigned long long*)grp_ctl);
       // the look-back pass over grp_ctl[1] rows: 0 unless k_subruns fell back

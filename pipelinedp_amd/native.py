@@ -38,6 +38,9 @@ DEBUG_THIN2 = 67108864  # K4 on: the LDS-staged k_thin2 instead of k_thin (measu
 # second flag word (pdp_bound_params.reserved2)
 DEBUG2_OVERFLOW_FULL1 = 1  # a second overflow range already sets the "redo everything on the generic path" flag
 DEBUG2_FILTER_REC8 = 2  # L0 pre-filter bucket pass with 8-byte {pk, row index} records (measured slower, r06c)
+DEBUG2_NO_GROUP = 4  # survivor grouping by a second look-back pass instead of the LDS grouping (k_group)
+DEBUG2_GROUP_FALLBACK = 8  # the LDS grouping hands every sub-run to that look-back pass (device-side fallback)
+DEBUG2_NO_CLASS_SPLIT = 16  # bucket pass without the low-level-first order inside a tile's bucket run
 DEBUG_NO_HOT_CACHE = 524288  # K2 without its hot-partition table (K4 off: LDS atomics cache; K4 on: K4Hot)
 
 c_i32, c_i64, c_u64, c_f64 = ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64, ctypes.c_double
