@@ -1944,7 +1944,7 @@ Layout layout_for(int64_t n, bool sweep = false, int64_t k4p = 0, bool variance 
   L.tag_lo = o; o += 256 * 4;
   L.keep = o; o += sweep ? 0 : align_up((size_t)std::max<int64_t>(n, 1) / 4 + 64, 256);  // k_filter keep bytes
   // survivor grouping (pdp_group.inc): per-bucket low-byte histogram, claimed run bases, sub-run table, ctl
-  L.grp = o; o += sweep ? 0 : align_up(256 * 256 * 4 + 256 * 8 + (size_t)kGrpSubruns * 8 + 16, 256);
+  L.grp = o; o += sweep ? 0 : align_up(256 * 256 * 4 + 256 * 8 + (size_t)kGrpSubruns * 8 + 32, 256);
   L.k4rep = o; o += k4p > 0 ? align_up((size_t)kK4Rep * kK4MaxPasses * 256 * 4, 256) : 0;
   L.k4s = o; o += k4p > 0 ? align_up((size_t)k4p * 20, 256) : 0;
   L.total = o;
@@ -2205,7 +2205,8 @@ int sort_recs(pdp_ctx* ctx, Rec* a, Rec* b, int64_t m, const KeySpec& ks, unsign
               unsigned long long* off, unsigned long long* counters, unsigned long long* status, size_t status_bytes,
               void* ws, hipStream_t stream, Rec** out, int stage = PDP_STAGE_GENERIC,
               const int64_t* soa_pid = nullptr, const int64_t* soa_pk = nullptr, const double* soa_val = nullptr,
-              const unsigned long long* m_dev = nullptr, int run_passes = -1) {
+              const unsigned long long* m_dev = nullptr, int run_passes = -1, bool hist_ready = false) {
+  // hist_ready: the caller filled `hist` (the pre-filter's survivor sort: k_filter_hist), no histogram pass
   // run_passes >= 0: histogram and offsets for all ks.passes, but only the first run_passes passes run
   // (the survivor grouping finishes the last one in LDS, pdp_group.inc)
   // soa_pk != null: the utility analysis' rows, packed by the histogram and the first pass themselves
@@ -2219,14 +2220,16 @@ int sort_recs(pdp_ctx* ctx, Rec* a, Rec* b, int64_t m, const KeySpec& ks, unsign
     HIP_TRY(zero_async(counters + kCtrTile0, (kNumCounters - kCtrTile0) * 8, stream));
     ctx->tile_slot = kCtrTile0;
   }
-  HIP_TRY(zero_async(hist, kMaxPasses * kHist * 8, stream));
+  if (!hist_ready) HIP_TRY(zero_async(hist, kMaxPasses * kHist * 8, stream));
   ProfScope prof_generic(ctx, stage, stream);
-  if (soa_pk)
+  if (hist_ready) {
+  } else if (soa_pk) {
     hipLaunchKernelGGL(k_histogram<2>, dim3(grid_for(m, kThreads, 2048)), dim3(kThreads), 0, stream, soa_pid, soa_pk,
                        (const Rec*)nullptr, m, ks, hist, counters, m_dev);
-  else
+  } else {
     hipLaunchKernelGGL(k_histogram<0>, dim3(grid_for(m, kThreads, 2048)), dim3(kThreads), 0, stream,
                        (const int64_t*)nullptr, (const int64_t*)nullptr, a, m, ks, hist, counters, m_dev);
+  }
   hipLaunchKernelGGL(k_offsets, dim3(1), dim3(kThreads), 0, stream, hist, off, ks.passes, m, counters,
                      (int)kCtrNGeneric, m_dev);
   Rec* src = a;
@@ -3271,13 +3274,18 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
     // Two passes: the second one's work is done by k_group in LDS (pdp_group.inc) -- unless a sub-run is
     // too long for it, which k_subruns decides on the device (the look-back pass then runs on every row).
     const bool group = k2.passes == 2 && !(bp->reserved2 & kDebug2NoGroup);
+    if (group) {  // the first pass's digit histogram is the sum of the filter's per-bucket ones (no read)
+      HIP_TRY(zero_async(hist, kMaxPasses * kHist * 8, stream));
+      hipLaunchKernelGGL(k_filter_hist, dim3(256), dim3(256), 0, stream, (const unsigned int*)shist, hist);
+    }
     int rc = sort_recs(ctx, sa, sb, n, k2, hist, off, counters, status, status_bytes, workspace, stream, &out,
-                       PDP_STAGE_SURVIVOR_SORT, nullptr, nullptr, nullptr, counters + kCtrNSurv, group ? 1 : -1);
+                       PDP_STAGE_SURVIVOR_SORT, nullptr, nullptr, nullptr, counters + kCtrNSurv, group ? 1 : -1,
+                       group);
     if (rc) return rc;
     if (group) {
       ProfScope ps(ctx, PDP_STAGE_SURVIVOR_GROUP, stream);
       Rec* dst = (out == sa) ? sb : sa;
-      HIP_TRY(zero_async(grp_ctl, 16, stream));
+      HIP_TRY(zero_async(grp_ctl, 24, stream));
       hipLaunchKernelGGL(k_subruns, dim3(256), dim3(256), 0, stream, (const unsigned int*)shist,
                          (const unsigned long long*)sbase, (const unsigned long long*)off,
                          (const unsigned long long*)(counters + kCtrNSurv), subruns, grp_ctl,
@@ -3285,7 +3293,14 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
       hipLaunchKernelGGL(k_group, dim3(4096), dim3(64 * kGrpBlockWaves), 0, stream, (const Rec*)out, dst,
                          (const uint2*)subruns, (int)kGrpSubruns, k2.shift[1], k2.bits[1],
                          (const unsigned long long*)grp_ctl);
-      // the look-back pass over grp_ctl[1] rows: 0 unless k_subruns fell back
+      // the look-back pass over grp_ctl[1] rows: 0 unless k_subruns fell back (then its digit histogram and
+      // offsets first; the row count k_offsets derives goes to grp_ctl[2], not to K2's counter)
+      HIP_TRY(zero_async(hist, kMaxPasses * kHist * 8, stream));
+      hipLaunchKernelGGL(k_histogram<0>, dim3(grid_for(n, kThreads, 2048)), dim3(kThreads), 0, stream,
+                         (const int64_t*)nullptr, (const int64_t*)nullptr, (const Rec*)out, n, k2, hist, counters,
+                         (const unsigned long long*)(grp_ctl + 1));
+      hipLaunchKernelGGL(k_offsets, dim3(1), dim3(kThreads), 0, stream, hist, off, k2.passes, n, grp_ctl, 2,
+                         (const unsigned long long*)(grp_ctl + 1));
       next_epoch_dev(ctx, stream, status, grp_ctl + 1, 0, true);
       const int occ = dev_occ(ctx->cur_debug);
       auto dev_kern = occ == 2 ? k_onesweep_dev<2> : occ == 4 ? k_onesweep_dev<4> : k_onesweep_dev<3>;
