@@ -166,6 +166,28 @@ def test_prefilter_matches_unfiltered_at_scale(ex, L0, Linf, z, rows_per_pid):
             np.testing.assert_array_equal(a, b)
 
 
+@pytest.mark.parametrize("flags2", [0, 16])
+def test_prefilter_with_non_public_rows(ex, flags2):
+    """The pre-filter's bucket pass places a non-public row (pk < 0) in its privacy id's bucket with a
+    "dropped" tag (k_filter never keeps it) and orders each tile's bucket run by level class.  With 30 %
+    of the rows non-public, the oracle's accumulators bit for bit (also without the class split:
+    NO_CLASS_SPLIT)."""
+    n, U, P = 1 << 21, 20000, 30000
+    pid, pk, val = o.synth_rows(n, U, P, seed=41, zipf_s=1.1, value_lo=-5, value_hi=15)
+    rng = np.random.default_rng(41)
+    pk = np.where(rng.random(n) < 0.3, -1, pk)
+    for L0, Linf in ((2, 2), (5, 3)):
+        bp = o.BoundParams(L0, Linf, 0.0, 10.0)
+        mask = 1 | 2 | 4 | 16
+        _, _, rc, cnt, x, _ = run_gpu(ex, pid, pk, val, U, P, bp, mask, seed=23, debug_flags=FORCE_FILTER,
+                                      debug_flags2=flags2)
+        st = ex.stats()
+        assert st.filter_rows > 0 and st.kept_rows_in == int((pk >= 0).sum())
+        ref = o.bound_and_accumulate(pid, pk, val, P, bp, "hash", seed=23)
+        check_acc(ref, rc, cnt, x, None, mask, val, bp)
+        assert st.filter_rows == int(o.prefilter_survivors(pid, pk, 23, L0).sum())
+
+
 @pytest.mark.parametrize("L0,Linf,rows_per_pid,zipf", [(1, 1, 4, 0.0), (2, 3, 6, 1.1), (4, 2, 5, 1.3),
                                                          (8, 4, 16, 0.0)])
 def test_survivor_grouping_forms_bitwise_equal(ex, L0, Linf, rows_per_pid, zipf):
