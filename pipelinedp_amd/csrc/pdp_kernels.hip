@@ -3237,6 +3237,28 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
   int n_slot = kCtrNKept;  // counter holding the number of rows in `sorted`
   uint64_t n_sorted = (uint64_t)n;  // upper bound of that number (grid sizes)
   if (fpl.on) {
+    // The survivors' grouping key: the low low_bits bits of the pid.  9..16 bits: a look-back pass on
+    // the low (low_bits - 8) bits, then the LDS grouping by the remaining 8 (pdp_group.inc) -- the first
+    // pass takes the narrower digit so that the (bucket, digit) sub-runs stay ~1K rows when the buckets
+    // are narrow (a rank's share of c3 at 8 GPUs: 13 bits -> 5 + 8, 8192 sub-runs instead of 65536).
+    // Otherwise 8-bit look-back passes.
+    KeySpec k2 = ks;
+    k2.passes = 0;
+    const bool group = fpl.low_bits >= 9 && fpl.low_bits <= 16 && !(bp->reserved2 & kDebug2NoGroup);
+    if (group) {
+      k2.shift[0] = 0;
+      k2.bits[0] = fpl.low_bits - 8;
+      k2.shift[1] = fpl.low_bits - 8;
+      k2.bits[1] = 8;
+      k2.passes = 2;
+    } else {
+      for (int sh = 0; sh < fpl.low_bits; sh += 8) {
+        k2.shift[k2.passes] = sh;
+        k2.bits[k2.passes] = std::min(8, fpl.low_bits - sh);
+        ++k2.passes;
+      }
+    }
+    const int nd0 = 1 << k2.bits[0];  // first-pass digits (sub-runs: nd0 x 256 buckets)
     // K1f: survivors of the bucket-sorted rows -> spare (input order per pid kept)
     HIP_TRY(zero_async(counters + kCtrNSurv, 8, stream));
     unsigned int* shist = (unsigned int*)(ws + L.grp);
@@ -3251,7 +3273,8 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
                          dim3(256), dim3(kFiltThreads), 0, stream, sorted, cols->value, tags, tag_lo, spare,
                          (uint8_t*)(ws + L.keep), off, counters,
                          (int)kCtrNKept, (int)kCtrNSurv, (int)bp->max_partitions_contributed,
-                         (sp.debug & kDebugFilterTiming) != 0, shist, sbase);
+                         (sp.debug & kDebugFilterTiming) != 0, shist, sbase, (uint32_t)U,
+                         (uint32_t)(nd0 - 1));
     }
     HIP_TRY(hipGetLastError());
     // Survivors stably by pid & (2^low_bits - 1) only.  That groups every pid: within a bucket the
@@ -3259,13 +3282,6 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
     // from different buckets stay in the order of their buckets' runs, because k_filter writes each
     // bucket's survivors as ONE contiguous run.  (No bucket-digit pass: the order of the pids does
     // not matter to K2, only their grouping.)
-    KeySpec k2 = ks;
-    k2.passes = 0;
-    for (int sh = 0; sh < fpl.low_bits; sh += 8) {
-      k2.shift[k2.passes] = sh;
-      k2.bits[k2.passes] = std::min(8, fpl.low_bits - sh);
-      ++k2.passes;
-    }
     ctx->stats.sort_passes += k2.passes;
     // the survivor count stays on the device (counters[kCtrNSurv]): the sort and K2 are sized by n
     Rec* sa = spare;
@@ -3273,10 +3289,9 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
     Rec* out = nullptr;
     // Two passes: the second one's work is done by k_group in LDS (pdp_group.inc) -- unless a sub-run is
     // too long for it, which k_subruns decides on the device (the look-back pass then runs on every row).
-    const bool group = k2.passes == 2 && !(bp->reserved2 & kDebug2NoGroup);
     if (group) {  // the first pass's digit histogram is the sum of the filter's per-bucket ones (no read)
       HIP_TRY(zero_async(hist, kMaxPasses * kHist * 8, stream));
-      hipLaunchKernelGGL(k_filter_hist, dim3(256), dim3(256), 0, stream, (const unsigned int*)shist, hist);
+      hipLaunchKernelGGL(k_filter_hist, dim3(nd0), dim3(256), 0, stream, (const unsigned int*)shist, hist);
     }
     int rc = sort_recs(ctx, sa, sb, n, k2, hist, off, counters, status, status_bytes, workspace, stream, &out,
                        PDP_STAGE_SURVIVOR_SORT, nullptr, nullptr, nullptr, counters + kCtrNSurv, group ? 1 : -1,
@@ -3286,12 +3301,12 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
       ProfScope ps(ctx, PDP_STAGE_SURVIVOR_GROUP, stream);
       Rec* dst = (out == sa) ? sb : sa;
       HIP_TRY(zero_async(grp_ctl, 24, stream));
-      hipLaunchKernelGGL(k_subruns, dim3(256), dim3(256), 0, stream, (const unsigned int*)shist,
+      hipLaunchKernelGGL(k_subruns, dim3(nd0), dim3(256), 0, stream, (const unsigned int*)shist,
                          (const unsigned long long*)sbase, (const unsigned long long*)off,
                          (const unsigned long long*)(counters + kCtrNSurv), subruns, grp_ctl,
                          (bp->reserved2 & kDebug2GroupFallback) ? 1u : kGrpBig);
       hipLaunchKernelGGL(k_group, dim3(4096), dim3(64 * kGrpBlockWaves), 0, stream, (const Rec*)out, dst,
-                         (const uint2*)subruns, (int)kGrpSubruns, k2.shift[1], k2.bits[1],
+                         (const uint2*)subruns, nd0 * 256, k2.shift[1], k2.bits[1],
                          (const unsigned long long*)grp_ctl);
       // the look-back pass over grp_ctl[1] rows: 0 unless k_subruns fell back (then its digit histogram and
       // offsets first; the row count k_offsets derives goes to grp_ctl[2], not to K2's counter)
