@@ -3241,15 +3241,21 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
     // the low (low_bits - 8) bits, then the LDS grouping by the remaining 8 (pdp_group.inc) -- the first
     // pass takes the narrower digit so that the (bucket, digit) sub-runs stay ~1K rows when the buckets
     // are narrow (a rank's share of c3 at 8 GPUs: 13 bits -> 5 + 8, 8192 sub-runs instead of 65536).
+    // The first pass widens (up to 8 bits) while the expected survivors (~1.7 rows per kept
+    // (pid, partition) pair, U x L0 pairs: measured 1.66-1.7 at c2/c3) would make the average sub-run
+    // longer than ~1150 rows, i.e. past k_group's register/LDS stage (c2: 12 bits -> 6 + 6, not 4 + 8).
     // Otherwise 8-bit look-back passes.
     KeySpec k2 = ks;
     k2.passes = 0;
     const bool group = fpl.low_bits >= 9 && fpl.low_bits <= 16 && !(bp->reserved2 & kDebug2NoGroup);
     if (group) {
+      const double est = std::min((double)n, 1.7 * (double)U * (double)bp->max_partitions_contributed);
+      int b1 = fpl.low_bits - 8;
+      while (b1 < 8 && est > 1150.0 * 256.0 * (double)(1 << b1)) ++b1;
       k2.shift[0] = 0;
-      k2.bits[0] = fpl.low_bits - 8;
-      k2.shift[1] = fpl.low_bits - 8;
-      k2.bits[1] = 8;
+      k2.bits[0] = b1;
+      k2.shift[1] = b1;
+      k2.bits[1] = fpl.low_bits - b1;
       k2.passes = 2;
     } else {
       for (int sh = 0; sh < fpl.low_bits; sh += 8) {
