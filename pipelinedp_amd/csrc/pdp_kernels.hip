@@ -174,6 +174,9 @@ struct KeySpec {
   // the pre-filter's bucket pass (TAG): within a tile's run of a bucket, rows of sketch level <= tau come
   // first (a stable split by one class bit; the order within a (pid, pk) group -- one level -- is kept)
   int tau;
+  // ... and in every odd tile they come LAST: the class-0 rows of tiles 2i+1 and 2i+2 then sit side by side
+  // in the bucket's region, so k_filter's survivor gather reads about half as many lines
+  int flip;
   int prof;  // accumulate per-phase s_memtime cycles of k_onesweep (kDebugSweepStamps)
   int ablate;  // kDebugNoLookback / kDebugLinearWrite (timing ablations, results invalid)
   int xcd_remap;  // reduce-then-scan passes: blocks sharing an XCD take one contiguous run of tiles
@@ -903,7 +906,7 @@ __device__ __forceinline__ bool onesweep_body(
           } else {
             const uint32_t lv = filt_level(filt_prio(ks.seed, ks.pid_base + r[k].pid, r[k].pk));
             r[k].pid = (d << 22) | ((r[k].pid - s_lo[d]) << 5) | lv;
-            d = 2u * d + (lv > (uint32_t)ks.tau ? 1u : 0u);
+            d = 2u * d + ((lv > (uint32_t)ks.tau ? 1u : 0u) ^ ((uint32_t)tile & (uint32_t)ks.flip));
           }
         }
       } else {
@@ -3164,10 +3167,12 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
     // priorities; a poor tau costs only speed (a (pid, pk) group has one level, so its rows keep their
     // input order whatever tau is).
     {
-      const double q = 3.0 * (double)bp->max_partitions_contributed * (double)U / (double)std::max<int64_t>(n, 1);
+      const double slack = (double)env_int("PDP_TAU_SLACK10", 30) / 10.0;  // experiment builds only
+      const double q = slack * (double)bp->max_partitions_contributed * (double)U / (double)std::max<int64_t>(n, 1);
       int tau = q >= 1.0 ? 31 : (int)std::floor(31.0 + 4.0 * std::log2(q));
       tau = std::min(31, std::max(0, tau));
       ks.tau = (bp->reserved2 & kDebug2NoClassSplit) ? 31 : tau;
+      ks.flip = env_int("PDP_CLASS_FLIP", 1) ? 1 : 0;  // experiment builds only (the shipped library: 1)
     }
     ks.passes = 1;
     ks.shift[0] = 64;
