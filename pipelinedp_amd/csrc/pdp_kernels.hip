@@ -280,6 +280,7 @@ constexpr int kDebug2FilterRec8 = 2;
 constexpr int kDebug2NoGroup = 4;        // survivor grouping by the round-5 second look-back pass, not k_group
 constexpr int kDebug2GroupFallback = 8;  // k_subruns hands every grouping to the look-back pass (kGrpBig = 1)
 constexpr int kDebug2NoClassSplit = 16;  // bucket pass: no low-level-first order within a tile's bucket run
+constexpr int kDebug2ThinChunk2048 = 32;  // k_thin's 2048-row chunks whatever the expected survivor count
 // Timing ablations whose results are invalid: accepted only by a -DPDP_DEBUG_BUILD library.
 constexpr int kAblationFlags = kDebugSortOnly | kDebugNoLookback | kDebugLinearWrite | kDebugNoScatter |
                                kDebugNoAtomics | kDebugWalkOnly | kDebugNoLinf | kDebugNoSums | kDebugFilterTiming;
@@ -3391,7 +3392,11 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
     ProfScope ps(ctx, PDP_STAGE_BUCKETS, stream);
     if (thin) {
       const bool v2 = thin2;
-      const int64_t chunk = v2 ? kThin2Chunk : kThinChunk;
+      // 2048-row chunks when many survivors are expected (c3: K2 1.88 -> 1.73 ms), 1024 for a rank's share
+      // (8-way: 0.35 vs 0.38 ms); the estimate is the survivor grouping's (1.7 rows per kept pair)
+      const double est_surv = std::min((double)n, 1.7 * (double)U * (double)bp->max_partitions_contributed);
+      const int64_t chunk = v2 ? kThin2Chunk : (est_surv >= 3e7 || (bp->reserved2 & kDebug2ThinChunk2048)
+                                                          ? kThinChunkMax : kThinChunk);
       const int64_t waves = ((int64_t)n_sorted + chunk - 1) / chunk;
       // LDS partition cache on: the Zipf-head pairs' HBM atomics otherwise dominate (c3: K2 8.1 -> 3.4 ms);
       // K4 writes pair records instead of atomics, no cache
@@ -3399,8 +3404,8 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
       const int64_t blocks =
           std::max<int64_t>(1, std::min<int64_t>((waves + 3) / 4, (sp.debug & kDebugOddGrid) ? 7 : kThinMaxBlocks));
       const int64_t l0 = bp->max_partitions_contributed;
-      auto kern = v2 ? (l0 <= 1 ? k_thin2<1> : l0 <= 2 ? k_thin2<2> : l0 <= 4 ? k_thin2<4> : k_thin2<8>)
-                : k4hot ? (l0 <= 1 ? k_thin<false, 1, false, true> : l0 <= 2 ? k_thin<false, 2, false, true>
+      auto kern2 = l0 <= 1 ? k_thin2<1> : l0 <= 2 ? k_thin2<2> : l0 <= 4 ? k_thin2<4> : k_thin2<8>;
+      auto kern = k4hot ? (l0 <= 1 ? k_thin<false, 1, false, true> : l0 <= 2 ? k_thin<false, 2, false, true>
                            : l0 <= 4 ? k_thin<false, 4, false, true> : k_thin<false, 8, false, true>)
                 : k4_compact ? (l0 <= 1 ? k_thin<false, 1, true> : l0 <= 2 ? k_thin<false, 2, true>
                                 : l0 <= 4 ? k_thin<false, 4, true> : k_thin<false, 8, true>)
@@ -3408,8 +3413,12 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
                 : l0 <= 2 ? (tcache ? k_thin<true, 2> : k_thin<false, 2>)
                 : l0 <= 4 ? (tcache ? k_thin<true, 4> : k_thin<false, 4>)
                           : (tcache ? k_thin<true, 8> : k_thin<false, 8>);
-      hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), 0, stream, sorted, counters, n_slot, sp, acc, ov, big,
-                         (int)bp->debug_force_fallback);
+      if (v2)
+        hipLaunchKernelGGL(kern2, dim3((unsigned)blocks), dim3(256), 0, stream, sorted, counters, n_slot, sp, acc, ov,
+                           big, (int)bp->debug_force_fallback);
+      else
+        hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), 0, stream, sorted, counters, n_slot, sp, acc, ov,
+                           big, (int)bp->debug_force_fallback, (int)chunk);
     } else if (lean) {
       const int64_t waves = ((int64_t)n_sorted + kLeanChunk - 1) / kLeanChunk;
       int64_t max_blocks = kLeanMaxBlocks;

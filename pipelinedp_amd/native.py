@@ -41,6 +41,7 @@ DEBUG2_FILTER_REC8 = 2  # L0 pre-filter bucket pass with 8-byte {pk, row index} 
 DEBUG2_NO_GROUP = 4  # survivor grouping by a second look-back pass instead of the LDS grouping (k_group)
 DEBUG2_GROUP_FALLBACK = 8  # the LDS grouping hands every sub-run to that look-back pass (device-side fallback)
 DEBUG2_NO_CLASS_SPLIT = 16  # bucket pass without the low-level-first order inside a tile's bucket run
+DEBUG2_THIN_CHUNK_2048 = 32  # K2 k_thin with 2048-row wave chunks whatever the expected survivor count
 DEBUG_NO_HOT_CACHE = 524288  # K2 without its hot-partition table (K4 off: LDS atomics cache; K4 on: K4Hot)
 
 c_i32, c_i64, c_u64, c_f64 = ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64, ctypes.c_double

@@ -156,10 +156,11 @@ def test_prefilter_matches_unfiltered_at_scale(ex, L0, Linf, z, rows_per_pid):
     np.testing.assert_allclose(x, x2, rtol=1e-9, atol=1e-9)
     ref = o.bound_and_accumulate(pid, pk, val, P, bp, "hash", seed=9)
     check_acc(ref, rc, cnt, x, None, mask, val, bp)
-    # the 8-byte bucket records (values gathered by row index, debug2 FILTER_REC8) and the bucket pass
-    # without its low-level-first order within a tile's bucket run (debug2 NO_CLASS_SPLIT): the same
-    # survivors and accumulators, bit for bit
-    for flags2 in (2, 16):
+    # the 8-byte bucket records (values gathered by row index, debug2 FILTER_REC8), the bucket pass
+    # without its low-level-first order within a tile's bucket run (debug2 NO_CLASS_SPLIT) and K2's
+    # 2048-row chunks (debug2 THIN_CHUNK_2048, the c3-sized choice): the same survivors and
+    # accumulators, bit for bit
+    for flags2 in (2, 16, 32):
         _, _, rc3, cnt3, x3, _ = run_gpu(ex, pid, pk, val, U, P, bp, mask, seed=9, debug_flags2=flags2)
         assert ex.stats().filter_rows == surv
         for a, b in ((rc, rc3), (cnt, cnt3), (x, x3)):
