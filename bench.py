@@ -139,9 +139,9 @@ def stage_bytes(stage, n_in, n_kept, P, nfields, survivors=0, survivor_passes=0,
         "onesweep_rest": 32 * n_kept,  # read + write 16-B records
         # tags twice (sketch, count) + keep bytes written and read; per survivor its 16-B record read and written
         "filter": 8.5 * n_kept + 32 * survivors,
-        # histogram read + per look-back pass (read + write); with the LDS grouping (survivor_group) the
-        # second pass's read + write moves to that stage
-        "survivor_sort": survivors * (16 + 32 * (survivor_passes - (1 if grouped else 0))),
+        # histogram read + per look-back pass (read + write) after the first grouping step, which k_filter
+        # does while compacting (round 6); with the LDS grouping (survivor_group) there is no such pass
+        "survivor_sort": survivors * (16 + 32 * max(survivor_passes - 1 - (1 if grouped else 0), 0)),
         "survivor_group": 32 * survivors,
         "buckets": 16 * sorted_rows + (32 if y_slots else 16) * slots,  # read 16-B records once (+ K4: write the pair slots)
         "pair_pass": 16 * slots + 16 * pairs + 32 * pairs * max(kpasses - 1, 0),

@@ -1948,7 +1948,7 @@ Layout layout_for(int64_t n, bool sweep = false, int64_t k4p = 0, bool variance 
   L.tag_lo = o; o += 256 * 4;
   L.keep = o; o += sweep ? 0 : align_up((size_t)std::max<int64_t>(n, 1) / 4 + 64, 256);  // k_filter keep bytes
   // survivor grouping (pdp_group.inc): per-bucket low-byte histogram, claimed run bases, sub-run table, ctl
-  L.grp = o; o += sweep ? 0 : align_up(256 * 256 * 4 + 256 * 8 + (size_t)kGrpSubruns * 8 + 32, 256);
+  L.grp = o; o += sweep ? 0 : align_up((size_t)kGrpSubruns * 8 + 32, 256);
   L.k4rep = o; o += k4p > 0 ? align_up((size_t)kK4Rep * kK4MaxPasses * 256 * 4, 256) : 0;
   L.k4s = o; o += k4p > 0 ? align_up((size_t)k4p * 20, 256) : 0;
   L.total = o;
@@ -3270,14 +3270,13 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
         ++k2.passes;
       }
     }
-    const int nd0 = 1 << k2.bits[0];  // first-pass digits (sub-runs: nd0 x 256 buckets)
-    // K1f: survivors of the bucket-sorted rows -> spare (input order per pid kept)
+    const int nd0 = 1 << k2.bits[0];  // the filter's digits d0 (sub-runs: nd0 x 256 buckets)
+    // K1f: survivors of the bucket-sorted rows -> spare, each bucket's run ordered by d0 = the first
+    // grouping step (input order per pid kept)
     HIP_TRY(zero_async(counters + kCtrNSurv, 8, stream));
-    unsigned int* shist = (unsigned int*)(ws + L.grp);
-    unsigned long long* sbase = (unsigned long long*)(shist + 256 * 256);
-    uint2* subruns = (uint2*)(sbase + 256);
+    uint2* subruns = (uint2*)(ws + L.grp);
     unsigned long long* grp_ctl = (unsigned long long*)(subruns + kGrpSubruns);
-    HIP_TRY(zero_async(shist, 256 * 256 * 4 + 256 * 8, stream));  // buckets without rows claim nothing
+    HIP_TRY(zero_async(grp_ctl, 24, stream));
     {
       ProfScope ps(ctx, PDP_STAGE_FILTER, stream);
       hipLaunchKernelGGL(fpl.half ? (rec16 ? k_filter<true, false> : k_filter<true, true>)
@@ -3285,43 +3284,31 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
                          dim3(256), dim3(kFiltThreads), 0, stream, sorted, cols->value, tags, tag_lo, spare,
                          (uint8_t*)(ws + L.keep), off, counters,
                          (int)kCtrNKept, (int)kCtrNSurv, (int)bp->max_partitions_contributed,
-                         (sp.debug & kDebugFilterTiming) != 0, shist, sbase, (uint32_t)U,
-                         (uint32_t)(nd0 - 1));
+                         (sp.debug & kDebugFilterTiming) != 0, group ? subruns : (uint2*)nullptr, grp_ctl,
+                         (bp->reserved2 & kDebug2GroupFallback) ? 1u : kGrpBig, (uint32_t)U, (uint32_t)(nd0 - 1));
     }
     HIP_TRY(hipGetLastError());
     // Survivors stably by pid & (2^low_bits - 1) only.  That groups every pid: within a bucket the
     // ids are distinct mod 2^low_bits (a bucket spans <= 2^low_bits ids), and rows of equal low bits
     // from different buckets stay in the order of their buckets' runs, because k_filter writes each
     // bucket's survivors as ONE contiguous run.  (No bucket-digit pass: the order of the pids does
-    // not matter to K2, only their grouping.)
+    // not matter to K2, only their grouping.)  The filter did the first step (d0); the rest is k_group
+    // (9..16 low bits) or look-back passes on the remaining bytes.
     ctx->stats.sort_passes += k2.passes;
-    // the survivor count stays on the device (counters[kCtrNSurv]): the sort and K2 are sized by n
     Rec* sa = spare;
     Rec* sb = sorted;
-    Rec* out = nullptr;
-    // Two passes: the second one's work is done by k_group in LDS (pdp_group.inc) -- unless a sub-run is
-    // too long for it, which k_subruns decides on the device (the look-back pass then runs on every row).
-    if (group) {  // the first pass's digit histogram is the sum of the filter's per-bucket ones (no read)
-      HIP_TRY(zero_async(hist, kMaxPasses * kHist * 8, stream));
-      hipLaunchKernelGGL(k_filter_hist, dim3(nd0), dim3(256), 0, stream, (const unsigned int*)shist, hist);
-    }
-    int rc = sort_recs(ctx, sa, sb, n, k2, hist, off, counters, status, status_bytes, workspace, stream, &out,
-                       PDP_STAGE_SURVIVOR_SORT, nullptr, nullptr, nullptr, counters + kCtrNSurv, group ? 1 : -1,
-                       group);
-    if (rc) return rc;
+    Rec* out = sa;
+    // K2's row count (the survivors), and the fallback pass's (the survivors if a sub-run was too long)
+    hipLaunchKernelGGL(k_grp_count, dim3(1), dim3(64), 0, stream, counters, grp_ctl);
     if (group) {
       ProfScope ps(ctx, PDP_STAGE_SURVIVOR_GROUP, stream);
-      Rec* dst = (out == sa) ? sb : sa;
-      HIP_TRY(zero_async(grp_ctl, 24, stream));
-      hipLaunchKernelGGL(k_subruns, dim3(nd0), dim3(256), 0, stream, (const unsigned int*)shist,
-                         (const unsigned long long*)sbase, (const unsigned long long*)off,
-                         (const unsigned long long*)(counters + kCtrNSurv), subruns, grp_ctl,
-                         (bp->reserved2 & kDebug2GroupFallback) ? 1u : kGrpBig);
+      Rec* dst = sb;
       hipLaunchKernelGGL(k_group, dim3(4096), dim3(64 * kGrpBlockWaves), 0, stream, (const Rec*)out, dst,
                          (const uint2*)subruns, nd0 * 256, k2.shift[1], k2.bits[1],
                          (const unsigned long long*)grp_ctl);
-      // the look-back pass over grp_ctl[1] rows: 0 unless k_subruns fell back (then its digit histogram and
-      // offsets first; the row count k_offsets derives goes to grp_ctl[2], not to K2's counter)
+      // the look-back pass over grp_ctl[1] rows: 0 unless a sub-run was too long for k_group (then its
+      // digit histogram and offsets first; the row count k_offsets derives goes to grp_ctl[2], not to K2's
+      // counter)
       HIP_TRY(zero_async(hist, kMaxPasses * kHist * 8, stream));
       hipLaunchKernelGGL(k_histogram<0>, dim3(grid_for(n, kThreads, 2048)), dim3(kThreads), 0, stream,
                          (const int64_t*)nullptr, (const int64_t*)nullptr, (const Rec*)out, n, k2, hist, counters,
@@ -3339,6 +3326,16 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
                          (const uint32_t*)nullptr, (const Rec*)nullptr, (int64_t)INT64_MAX);
       HIP_TRY(hipGetLastError());
       out = dst;
+    } else if (k2.passes > 1) {  // look-back passes on the bytes above d0
+      KeySpec k3 = k2;
+      k3.passes = k2.passes - 1;
+      for (int p = 0; p < k3.passes; ++p) {
+        k3.shift[p] = k2.shift[p + 1];
+        k3.bits[p] = k2.bits[p + 1];
+      }
+      int rc = sort_recs(ctx, sa, sb, n, k3, hist, off, counters, status, status_bytes, workspace, stream, &out,
+                         PDP_STAGE_SURVIVOR_SORT, nullptr, nullptr, nullptr, counters + kCtrNSurv, -1, false);
+      if (rc) return rc;
     }
     sorted = out;
     spare = (out == sa) ? sb : sa;

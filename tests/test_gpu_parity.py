@@ -193,10 +193,10 @@ def test_prefilter_with_non_public_rows(ex, flags2):
                                                          (8, 4, 16, 0.0)])
 def test_survivor_grouping_forms_bitwise_equal(ex, L0, Linf, rows_per_pid, zipf):
     """Privacy-id buckets wider than 256 ids (here U = 2^19: 2048 ids per bucket, 11 low bits) take two
-    survivor-grouping steps: the look-back pass on the low byte, then the LDS grouping of each (bucket,
-    low byte) sub-run (k_subruns + k_group, round 6).  Against the round-5 second look-back pass
-    (debug2 NO_GROUP) and the device-side fallback that hands every sub-run to that pass (debug2
-    GROUP_FALLBACK): identical accumulators, bit for bit, and the oracle's."""
+    survivor-grouping steps: k_filter writes each bucket's survivors ordered by the low digit, then the
+    LDS grouping of each (bucket, low digit) sub-run (k_group, round 6).  Against look-back passes on the
+    remaining bits (debug2 NO_GROUP) and the device-side fallback that hands every sub-run to the
+    look-back pass (debug2 GROUP_FALLBACK): identical accumulators, bit for bit, and the oracle's."""
     n, P = 1 << 21, 50000
     U = 1 << 19 if rows_per_pid < 16 else 1 << 17
     pid, pk, val = o.synth_rows(n, U, P, seed=600 + L0, zipf_s=zipf, value_lo=-5, value_hi=15)

@@ -30,7 +30,7 @@ STAGE_OF = {"k_histogram_tiles": "histogram", "k_bucket_pass": "onesweep_first",
             "k_segments_big": "buckets", "k4_fill_ranges": "buckets", "k_pair_pass": "pair_pass",
             "k_pair_pass12_first": "pair_pass", "k_pair_pass12": "pair_pass", "k4_offsets": "pair_pass", "k4_set_counter": "pair_pass", "k4_reduce": "reduce",
             "k4_zero_shared": "reduce", "k4_finalize": "reduce", "k_release": "release",
-            "k_unpack_counts": "buckets", "k_subruns": "survivor_group", "k_group": "survivor_group",
+            "k_unpack_counts": "buckets", "k_subruns": "survivor_group", "k_grp_count": "survivor_group", "k_group": "survivor_group",
             "k_bucket_pass8": "onesweep_first"}
 # kernels of a records radix sort (the survivor sort after k_filter, or a pid-sort pass >= 1)
 # (round 5's device-sized survivor sort is k_onesweep_dev + k_status_clear: missing here until round 6, which
