@@ -167,6 +167,28 @@ def test_prefilter_matches_unfiltered_at_scale(ex, L0, Linf, z, rows_per_pid):
             np.testing.assert_array_equal(a, b)
 
 
+@pytest.mark.parametrize("U,P", [(1 << 14, 20), (1 << 18, 12)])
+def test_prefilter_dense_survivor_batches(ex, U, P):
+    """Few partitions per privacy id (P <= 20, L0 = 8): nearly every row survives the L0 pre-filter, so
+    k_filter's compaction batches overflow its LDS stage (direct stores) and a wave's 2048 rows need
+    several gather rounds (count pass first, round 6).  U = 2^14: 64 ids per bucket, the filter's digit
+    order is the whole grouping; U = 2^18: 1024 ids per bucket, k_group finishes it.  Against the
+    unfiltered path bit for bit and the oracle."""
+    n = 1 << 22
+    pid, pk, val = o.synth_rows(n, U, P, seed=700 + P, zipf_s=0.0, value_lo=-5, value_hi=15)
+    bp = o.BoundParams(8, 3, 0.0, 10.0)
+    mask = 1 | 2 | 4 | 16
+    _, _, rc, cnt, x, _ = run_gpu(ex, pid, pk, val, U, P, bp, mask, seed=31, debug_flags=FORCE_FILTER)
+    surv = ex.stats().filter_rows
+    assert surv > n // 2  # dense: most rows survive
+    assert surv == int(o.prefilter_survivors(pid, pk, 31, 8).sum())
+    _, _, rc2, cnt2, x2, _ = run_gpu(ex, pid, pk, val, U, P, bp, mask, seed=31, debug_flags=NO_FILTER)
+    for a, b in ((rc, rc2), (cnt, cnt2), (x, x2)):
+        np.testing.assert_array_equal(a, b)
+    ref = o.bound_and_accumulate(pid, pk, val, P, bp, "hash", seed=31)
+    check_acc(ref, rc, cnt, x, None, mask, val, bp)
+
+
 @pytest.mark.parametrize("flags2", [0, 16])
 def test_prefilter_with_non_public_rows(ex, flags2):
     """The pre-filter's bucket pass places a non-public row (pk < 0) in its privacy id's bucket with a
