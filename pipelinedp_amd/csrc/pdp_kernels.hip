@@ -3249,7 +3249,7 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
     // are narrow (a rank's share of c3 at 8 GPUs: 13 bits -> 5 + 8, 8192 sub-runs instead of 65536).
     // The first pass widens (up to 8 bits) while the expected survivors (~1.7 rows per kept
     // (pid, partition) pair, U x L0 pairs: measured 1.66-1.7 at c2/c3) would make the average sub-run
-    // longer than ~1150 rows, i.e. past k_group's register/LDS stage (c2: 12 bits -> 6 + 6, not 4 + 8).
+    // longer than ~1050 rows, near k_group's 1152-row register/LDS stage (c2: 12 bits -> 6 + 6, not 4 + 8).
     // Otherwise 8-bit look-back passes.
     KeySpec k2 = ks;
     k2.passes = 0;
@@ -3257,7 +3257,7 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
     if (group) {
       const double est = std::min((double)n, 1.7 * (double)U * (double)bp->max_partitions_contributed);
       int b1 = fpl.low_bits - 8;
-      while (b1 < 8 && est > 1150.0 * 256.0 * (double)(1 << b1)) ++b1;
+      while (b1 < 8 && est > 1050.0 * 256.0 * (double)(1 << b1)) ++b1;
       k2.shift[0] = 0;
       k2.bits[0] = b1;
       k2.shift[1] = b1;
