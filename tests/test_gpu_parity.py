@@ -257,14 +257,18 @@ def test_full_width_privacy_ids_and_wide_partition_ids(ex):
     assert ex.stats().sort_passes == 4
 
 
+@pytest.mark.parametrize("U", [15_000_000, 20_000_000])
 @pytest.mark.parametrize("L0,Linf", [(1, 1), (4, 2), (8, 3)])
-def test_prefilter_half_sketch_wide_buckets(ex, L0, Linf):
+def test_prefilter_half_sketch_wide_buckets(ex, L0, Linf, U):
     """U = 1.5e7 privacy ids: buckets of ~58,600 ids, wider than the LDS
     holds at 32 bits per id, so the filter uses 16-bit sketches (2 levels
-    per octave).  20,000 ids spread over the whole range carry ~100 rows
-    each.  Survivors equal the restatement's; bounding equals the oracle."""
+    per octave).  U = 2e7: buckets of ~78,100 ids, 17 low bits -- the
+    filter's digit order on the low byte, then look-back passes on bits 8-16
+    (no LDS grouping).  20,000 ids spread over the whole range carry ~100
+    rows each.  Survivors equal the restatement's; bounding equals the
+    oracle."""
     rng = np.random.default_rng(11 + L0)
-    U, P, n = 15_000_000, 50_000, 1 << 21
+    P, n = 50_000, 1 << 21
     assert o.prefilter_sketch_bits(U) == 16
     ids = rng.choice(U, 20000, replace=False)
     pid = ids[rng.integers(0, len(ids), n)].astype(np.int64)
