@@ -468,7 +468,7 @@ enum {
   PDP_STAGE_ANALYSIS_SORT = 14, /* utility analysis: the (pk, pid) radix sort inside ANALYSIS_PAIRS */
   PDP_STAGE_ANALYSIS_AGGREGATE = 15, /* utility analysis: cross-partition aggregate error metrics */
   PDP_STAGE_ANALYSIS_SELECT = 16, /* utility analysis: Poisson-binomial keep probability (inside ANALYSIS_METRICS) */
-  PDP_STAGE_SURVIVOR_GROUP = 17, /* ABI 4: the survivors' last grouping step in LDS (k_subruns + k_group) */
+  PDP_STAGE_SURVIVOR_GROUP = 17, /* ABI 4: the survivors' last grouping step in LDS (k_group) */
   PDP_NUM_STAGES = 18,
 };
 int pdp_profile_enable(pdp_ctx* ctx, int enable);

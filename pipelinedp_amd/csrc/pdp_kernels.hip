@@ -278,7 +278,7 @@ constexpr int kDebug2OverflowFull1 = 1;     // a second overflow range already s
 // values by row index (round-6 experiment: bucket pass 9.13 -> 7.6 ms, filter 3.26 -> 5.2 ms: slower, r06c)
 constexpr int kDebug2FilterRec8 = 2;
 constexpr int kDebug2NoGroup = 4;        // survivor grouping by the round-5 second look-back pass, not k_group
-constexpr int kDebug2GroupFallback = 8;  // k_subruns hands every grouping to the look-back pass (kGrpBig = 1)
+constexpr int kDebug2GroupFallback = 8;  // k_filter hands every grouping to the look-back pass (kGrpBig = 1)
 constexpr int kDebug2NoClassSplit = 16;  // bucket pass: no low-level-first order within a tile's bucket run
 constexpr int kDebug2ThinChunk2048 = 32;  // k_thin's 2048-row chunks whatever the expected survivor count
 // Timing ablations whose results are invalid: accepted only by a -DPDP_DEBUG_BUILD library.
@@ -2210,7 +2210,7 @@ int sort_recs(pdp_ctx* ctx, Rec* a, Rec* b, int64_t m, const KeySpec& ks, unsign
               void* ws, hipStream_t stream, Rec** out, int stage = PDP_STAGE_GENERIC,
               const int64_t* soa_pid = nullptr, const int64_t* soa_pk = nullptr, const double* soa_val = nullptr,
               const unsigned long long* m_dev = nullptr, int run_passes = -1, bool hist_ready = false) {
-  // hist_ready: the caller filled `hist` (the pre-filter's survivor sort: k_filter_hist), no histogram pass
+  // hist_ready: the caller filled `hist` (no histogram pass; unused since k_filter orders the survivors)
   // run_passes >= 0: histogram and offsets for all ks.passes, but only the first run_passes passes run
   // (the survivor grouping finishes the last one in LDS, pdp_group.inc)
   // soa_pk != null: the utility analysis' rows, packed by the histogram and the first pass themselves
