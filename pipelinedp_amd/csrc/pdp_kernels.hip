@@ -3253,7 +3253,9 @@ int bound_impl(pdp_ctx* ctx, const pdp_columns* cols, const pdp_bound_params* bp
     // Otherwise 8-bit look-back passes.
     KeySpec k2 = ks;
     k2.passes = 0;
-    const bool group = fpl.low_bits >= 9 && fpl.low_bits <= 16 && !(bp->reserved2 & kDebug2NoGroup);
+    // (the sub-run table holds 32-bit starts: inputs of 2^32 rows or more -- as many possible survivors --
+    // take the look-back passes)
+    const bool group = fpl.low_bits >= 9 && fpl.low_bits <= 16 && n < (1ll << 32) && !(bp->reserved2 & kDebug2NoGroup);
     if (group) {
       const double est = std::min((double)n, 1.7 * (double)U * (double)bp->max_partitions_contributed);
       int b1 = fpl.low_bits - 8;
